@@ -1,0 +1,253 @@
+/*
+ * mh_kernel.h -- C ABI of the MI355X Metropolis-Hastings interior-layout sampler.
+ *
+ * Drop-in boundary for the reference DLL surface
+ *   KernelFolder/Kernel/Kernel.cu:873  extern "C" __declspec(dllexport) result* KernelWrapper(...)
+ * The eleven wire structs below are byte-identical to Kernel.cu:43-149 on x86-64 (sizes and
+ * offsets are static_assert-ed at the bottom of this header and again in the library).
+ *
+ * Ownership: KernelWrapper returns a host-malloc'd result[gridxDim]; every result[i].points
+ * points into ONE malloc'd point[gridxDim * nObjs] block (as Kernel.cu:928,970-981 does).
+ * Free it with KernelFreeResult(). On any error NULL is returned and KernelLastError()
+ * describes it (the reference calls exit() inside the host process, helper_cuda.h:985-994).
+ */
+#ifndef MH_KERNEL_H_
+#define MH_KERNEL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define MH_API __attribute__((visibility("default")))
+#else
+#define MH_API
+#endif
+
+/* ---- wire structs: Kernel.cu:43-149 ------------------------------------------------------ */
+
+typedef struct vertex { /* Kernel.cu:43-48 */
+    double x;
+    double y;
+    double z;
+} vertex;
+
+typedef struct rectangle { /* Kernel.cu:50-57; only point1Index (4 consecutive vertices) and
+                              SourceIndex (clearances only) are read, Kernel.cu:366-401,414 */
+    int point1Index;
+    int point2Index;
+    int point3Index;
+    int point4Index;
+    int SourceIndex;
+} rectangle;
+
+typedef struct positionAndRotation { /* Kernel.cu:59-72 */
+    double x;
+    double y;
+    double z;
+    double rotX;
+    double rotY;
+    double rotZ;
+#ifdef __cplusplus
+    bool frozen;
+#else
+    _Bool frozen;
+#endif
+    double length;
+    double width;
+} positionAndRotation;
+
+typedef struct targetRangeStruct { /* Kernel.cu:74-77 */
+    double targetRangeStart;
+    double targetRangeEnd;
+} targetRangeStruct;
+
+typedef struct relationshipStruct { /* Kernel.cu:79-85 */
+    targetRangeStruct TargetRange;
+    int SourceIndex;
+    int TargetIndex;
+    double DegreesOfAtrraction; /* spelling as in the reference; unused by the cost model */
+} relationshipStruct;
+
+typedef struct relationshipAngleStruct { /* Kernel.cu:87-92 */
+    double angleMin;
+    double angleMax;
+    int SourceIndex;
+    int TargetIndex;
+} relationshipAngleStruct;
+
+typedef struct Surface { /* Kernel.cu:94-117 */
+    int nObjs;
+    int nRelationships;
+    int nClearances;
+    float WeightFocalPoint;
+    float WeightPairWise;
+    float WeightVisualBalance;
+    float WeightSymmetry;
+    float WeightOffLimits;
+    float WeightClearance;
+    float WeightSurfaceArea;
+    double centroidX;
+    double centroidY;
+    double focalX;
+    double focalY;
+    double focalRot;
+} Surface;
+
+typedef struct gpuConfig { /* Kernel.cu:119-127 */
+    int gridxDim;   /* number of chains (one result per chain) */
+    int gridyDim;   /* unused, as in the reference (Kernel.cu:946-947) */
+    int blockxDim;  /* accepted and ignored: lanes per chain are chosen by the library */
+    int blockyDim;  /* unused */
+    int blockzDim;  /* unused */
+    int iterations; /* MH steps per chain */
+} gpuConfig;
+
+typedef struct point { /* Kernel.cu:129-132 */
+    float x, y, z, rotX, rotY, rotZ;
+} point;
+
+typedef struct resultCosts { /* Kernel.cu:134-144 */
+    float totalCosts;
+    float PairWiseCosts;
+    float VisualBalanceCosts;
+    float FocalPointCosts;
+    float SymmetryCosts;
+    float ClearanceCosts;
+    float OffLimitsCosts;
+    float SurfaceAreaCosts;
+} resultCosts;
+
+typedef struct result { /* Kernel.cu:146-149 */
+    point* points;
+    resultCosts costs;
+} result;
+
+/* ---- the reference export ---------------------------------------------------------------- */
+
+/* Replaces Kernel.cu:873-984. Same name, parameter order and types. Runs gpuCfg->gridxDim
+ * independent chains of gpuCfg->iterations MH steps each on the current HIP device and returns
+ * every chain's final current configuration. Seed: $MH_SEED if set, else time(NULL)
+ * (Kernel.cu:943). result[i].costs holds the cost components of that final configuration
+ * (the reference leaves them uninitialised, Kernel.cu:852-861). Blocking. */
+MH_API result* KernelWrapper(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                             positionAndRotation* cfg, rectangle* clearances,
+                             rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
+                             Surface* srf, gpuConfig* gpuCfg);
+
+/* ---- additive exports -------------------------------------------------------------------- */
+
+/* KernelWrapper with an explicit 64-bit seed (chain c draws from Philox4x32-10 key=seed,
+ * subsequence=c). Identical seeds give identical results. */
+MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                                   positionAndRotation* cfg, rectangle* clearances,
+                                   rectangle* offlimits, vertex* vertices,
+                                   vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg,
+                                   uint64_t seed);
+
+/* Frees a KernelWrapper result (the points block and the array). NULL is a no-op. */
+MH_API void KernelFreeResult(result* res);
+
+/* Text of the last error on the calling thread ("" if none). */
+MH_API const char* KernelLastError(void);
+
+/* Evaluates the reference cost model (Kernel.cu:516-550, OffLimits included in its component,
+ * excluded from totalCosts as at :547) for n_cfgs configurations of nObjs objects each, laid
+ * out back to back in cfgs, on the current device. Returns 0 on success. */
+MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationshipAngleStruct* rsa,
+                               const positionAndRotation* cfgs, int n_cfgs,
+                               const rectangle* clearances, const rectangle* offlimits,
+                               const vertex* vertices, const vertex* surfaceRectangle,
+                               const Surface* srf, resultCosts* out_costs);
+
+/* ---- session API: device-resident chains (bench, multi-GPU sharding, resumable runs) ----- */
+
+typedef struct mh_session mh_session;
+
+typedef struct mh_summary {
+    double sum_total;      /* sum over this session's chains of final totalCosts */
+    float best_total;      /* max totalCosts (MH maximises, Kernel.cu:706-713) */
+    int32_t pad;
+    int64_t best_chain;    /* GLOBAL chain id of the best chain (lowest id on ties) */
+    int64_t n_chains;
+    int64_t accepted;      /* accepted proposals over all chains and steps so far */
+} mh_summary;
+
+/* Uploads the room tables to `device` and initialises n_chains chains with global ids
+ * [chain_offset, chain_offset + n_chains): state := cfg, Philox(seed, subsequence = id),
+ * initial costs. Returns NULL on error. */
+MH_API mh_session* mh_session_create(const relationshipStruct* rss,
+                                     const relationshipAngleStruct* rsa,
+                                     const positionAndRotation* cfg, const rectangle* clearances,
+                                     const rectangle* offlimits, const vertex* vertices,
+                                     const vertex* surfaceRectangle, const Surface* srf,
+                                     int device, int64_t n_chains, int64_t chain_offset,
+                                     uint64_t seed);
+
+/* Enqueues `iterations` MH steps for every chain on `stream` (a hipStream_t; NULL = the
+ * session's own stream). Chains resume exactly: k runs of m steps == one run of k*m steps. */
+MH_API int mh_session_run(mh_session* s, int iterations, void* stream);
+
+/* Enqueues the final-state pass (OffLimits component, float points) on `stream`. */
+MH_API int mh_session_finalize(mh_session* s, void* stream);
+
+/* Synchronous copies of the finalised chains (either pointer may be NULL). */
+MH_API int mh_session_download(mh_session* s, point* out_points, resultCosts* out_costs);
+
+/* Reduces the finalised chains on the device to one mh_summary (synchronous). */
+MH_API int mh_session_summary(mh_session* s, mh_summary* out);
+
+/* Lanes per chain and chains per 256-thread workgroup the session's kernel uses. */
+MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain,
+                               int* chains_per_workgroup);
+
+MH_API void mh_session_destroy(mh_session* s);
+
+/* ---- diagnostics -------------------------------------------------------------------------- */
+
+/* The first n Philox words, uniforms (curand_uniform stand-in) and normals (curand_normal
+ * stand-in) that chain `subsequence` draws under `seed`, computed on the current device by the
+ * same device code the chains use (each stream restarted at draw 0). Returns 0 on success. */
+MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
+                        float* out_uniform, float* out_normal);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+/* ---- layout checks (x86-64 values recorded in SURVEY.md 8(b)) ---------------------------- */
+#ifdef __cplusplus
+#define MH_STATIC_ASSERT static_assert
+#else
+#define MH_STATIC_ASSERT _Static_assert
+#endif
+MH_STATIC_ASSERT(sizeof(vertex) == 24, "vertex");
+MH_STATIC_ASSERT(sizeof(rectangle) == 20, "rectangle");
+MH_STATIC_ASSERT(sizeof(positionAndRotation) == 72, "positionAndRotation");
+MH_STATIC_ASSERT(offsetof(positionAndRotation, rotZ) == 40, "rotZ");
+MH_STATIC_ASSERT(offsetof(positionAndRotation, frozen) == 48, "frozen");
+MH_STATIC_ASSERT(offsetof(positionAndRotation, length) == 56, "length");
+MH_STATIC_ASSERT(offsetof(positionAndRotation, width) == 64, "width");
+MH_STATIC_ASSERT(sizeof(targetRangeStruct) == 16, "targetRangeStruct");
+MH_STATIC_ASSERT(sizeof(relationshipStruct) == 32, "relationshipStruct");
+MH_STATIC_ASSERT(offsetof(relationshipStruct, SourceIndex) == 16, "rs.SourceIndex");
+MH_STATIC_ASSERT(offsetof(relationshipStruct, TargetIndex) == 20, "rs.TargetIndex");
+MH_STATIC_ASSERT(offsetof(relationshipStruct, DegreesOfAtrraction) == 24, "rs.Degrees");
+MH_STATIC_ASSERT(sizeof(relationshipAngleStruct) == 24, "relationshipAngleStruct");
+MH_STATIC_ASSERT(offsetof(relationshipAngleStruct, SourceIndex) == 16, "ra.SourceIndex");
+MH_STATIC_ASSERT(sizeof(Surface) == 80, "Surface");
+MH_STATIC_ASSERT(offsetof(Surface, WeightFocalPoint) == 12, "WeightFocalPoint");
+MH_STATIC_ASSERT(offsetof(Surface, WeightSurfaceArea) == 36, "WeightSurfaceArea");
+MH_STATIC_ASSERT(offsetof(Surface, centroidX) == 40, "centroidX");
+MH_STATIC_ASSERT(offsetof(Surface, focalRot) == 72, "focalRot");
+MH_STATIC_ASSERT(sizeof(gpuConfig) == 24, "gpuConfig");
+MH_STATIC_ASSERT(sizeof(point) == 24, "point");
+MH_STATIC_ASSERT(sizeof(resultCosts) == 32, "resultCosts");
+MH_STATIC_ASSERT(sizeof(result) == 40, "result");
+MH_STATIC_ASSERT(offsetof(result, costs) == 8, "result.costs");
+MH_STATIC_ASSERT(sizeof(mh_summary) == 40, "mh_summary");
+
+#endif /* MH_KERNEL_H_ */

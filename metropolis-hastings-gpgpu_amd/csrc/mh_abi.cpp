@@ -1,0 +1,654 @@
+// mh_abi.cpp -- the C ABI of libmhgpu.so: KernelWrapper (Kernel.cu:873-984) and friends.
+//
+// Host side of the drop-in boundary. It validates the wire structs (the reference validates
+// nothing and exits the host process on a CUDA error, helper_cuda.h:985-994), reduces the room
+// to per-object device constants, owns device memory per session, and shards a KernelWrapper
+// call over $MH_DEVICES (one host thread and one stream per device; chain c always draws from
+// Philox subsequence c, so results do not depend on the device count).
+
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mh_launch.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string& e) { g_last_error = e; }
+
+#define MH_TRY_HIP(expr)                                                                   \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess) {                                                            \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                  \
+            return false;                                                                  \
+        }                                                                                  \
+    } while (0)
+
+// Largest chunk of MH steps per launch: keeps one launch well under a second at N=64.
+constexpr int kStepsPerLaunch = 1000;
+
+struct Room {
+    mh::DevRoom rm{};
+    std::vector<mh::ObjConst> obj;
+    std::vector<mh::ClrConst> clr;
+    std::vector<mh::RelConst> rel;
+    std::vector<double> cfg0;  // [6][N]
+};
+
+mh::RectShape make_shape(const vertex* v) {
+    mh::RectShape s{};
+    s.v0x = (float)v[0].x;
+    s.xmin1 = std::min(v[1].x, std::min(v[2].x, v[3].x));
+    s.xmax = std::max(std::max(v[0].x, v[1].x), std::max(v[2].x, v[3].x));
+    s.ymin = std::min(std::min(v[0].y, v[1].y), std::min(v[2].y, v[3].y));
+    s.ymax = std::max(std::max(v[0].y, v[1].y), std::max(v[2].y, v[3].y));
+    return s;
+}
+
+bool validate(const relationshipStruct* rss, const relationshipAngleStruct* rsa,
+              const positionAndRotation* cfg, const rectangle* clearances,
+              const rectangle* offlimits, const vertex* vertices, const vertex* srect,
+              const Surface* srf) {
+    if (!srf) { set_error("srf is NULL"); return false; }
+    const int n = srf->nObjs, c = srf->nClearances, nr = srf->nRelationships;
+    char buf[160];
+    if (n < 1) { snprintf(buf, sizeof buf, "nObjs must be >= 1 (got %d)", n); set_error(buf); return false; }
+    if (c < 0 || c > n) {
+        snprintf(buf, sizeof buf, "nClearances must be in [0, nObjs] (got %d)", c);
+        set_error(buf);
+        return false;
+    }
+    if (nr < 0) { set_error("nRelationships must be >= 0"); return false; }
+    if (!cfg || !offlimits || !vertices || !srect) { set_error("NULL input array"); return false; }
+    if ((nr > 0 && (!rss || !rsa)) || (c > 0 && !clearances)) { set_error("NULL input array"); return false; }
+    const long nv = 4L * (c + n);
+    bool any_free = false;
+    for (int i = 0; i < n; ++i) {
+        const int p = offlimits[i].point1Index;
+        if (p < 0 || p + 3 >= nv) {
+            snprintf(buf, sizeof buf, "offlimits[%d].point1Index out of range", i);
+            set_error(buf);
+            return false;
+        }
+        if (!cfg[i].frozen) any_free = true;
+    }
+    if (!any_free) { set_error("every object is frozen (the reference never terminates)"); return false; }
+    for (int i = 0; i < c; ++i) {
+        const int p = clearances[i].point1Index, q = clearances[i].SourceIndex;
+        if (p < 0 || p + 3 >= nv) {
+            snprintf(buf, sizeof buf, "clearances[%d].point1Index out of range", i);
+            set_error(buf);
+            return false;
+        }
+        if (q < 0 || q >= n) {
+            snprintf(buf, sizeof buf, "clearances[%d].SourceIndex out of range", i);
+            set_error(buf);
+            return false;
+        }
+    }
+    for (int i = 0; i < nr; ++i) {
+        if (rss[i].SourceIndex < 0 || rss[i].SourceIndex >= n || rss[i].TargetIndex < 0 ||
+            rss[i].TargetIndex >= n || rsa[i].SourceIndex < 0 || rsa[i].SourceIndex >= n ||
+            rsa[i].TargetIndex < 0 || rsa[i].TargetIndex >= n) {
+            snprintf(buf, sizeof buf, "relationship %d index out of range", i);
+            set_error(buf);
+            return false;
+        }
+    }
+    return true;
+}
+
+// Host reduction of the room (every value computed exactly as the reference computes it on
+// each call; see mh_device.h for what each field replaces).
+bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rsa,
+                const positionAndRotation* cfg, const rectangle* clearances,
+                const rectangle* offlimits, const vertex* vertices, const vertex* srect,
+                const Surface* srf, Room& out) {
+    if (!validate(rss, rsa, cfg, clearances, offlimits, vertices, srect, srf)) return false;
+    const int n = srf->nObjs, c = srf->nClearances, nr = srf->nRelationships;
+    mh::DevRoom& rm = out.rm;
+    rm.n = n;
+    rm.c = c;
+    rm.r = nr;
+    rm.w_pw = srf->WeightPairWise;
+    rm.w_vb = srf->WeightVisualBalance;
+    rm.w_fp = srf->WeightFocalPoint;
+    rm.w_sym = srf->WeightSymmetry;
+    rm.w_ol = srf->WeightOffLimits;
+    rm.w_cl = srf->WeightClearance;
+    rm.w_sa = srf->WeightSurfaceArea;
+    rm.fxf = (float)srf->focalX;
+    rm.fyf = (float)srf->focalY;
+    rm.ux = (float)cos(srf->focalRot);  // Kernel.cu:290
+    rm.uy = (float)sin(srf->focalRot);  // Kernel.cu:291
+    rm.cxf = (float)(srf->centroidX / 2);
+    rm.cyf = (float)(srf->centroidY / 2);
+    double along = srf->focalX * rm.ux;
+    along = along + srf->focalY * rm.uy;
+    rm.along_f = along;
+    rm.two_focal_rot = 2 * srf->focalRot;
+
+    // Room box: minValue/maxValue(surfaceRectangle, 0, 0, 0), Kernel.cu:448-449,585-586.
+    double rminx = DBL_MAX, rminy = DBL_MAX, rmaxx = -DBL_MAX, rmaxy = -DBL_MAX;
+    for (int k = 0; k < 4; ++k) {
+        rminx = std::min(rminx, srect[k].x);
+        rminy = std::min(rminy, srect[k].y);
+        rmaxx = std::max(rmaxx, srect[k].x);
+        rmaxy = std::max(rmaxy, srect[k].y);
+    }
+    rm.rmin_x = rminx;
+    rm.rmin_y = rminy;
+    rm.rmax_x = rmaxx;
+    rm.rmax_y = rmaxy;
+    const float width = (float)(rmaxx - rminx);
+    const float height = (float)(rmaxy - rminy);
+    rm.sx = width / 16;
+    rm.sy = height / 16;
+    // Complement rectangles, Kernel.cu:343-364, rounded to float as the overlap sees them.
+    const double comp[4][4] = {{-DBL_MAX, -DBL_MAX, DBL_MAX, rminy},
+                               {-DBL_MAX, rminy, rminx, rmaxy},
+                               {-DBL_MAX, rmaxy, DBL_MAX, DBL_MAX},
+                               {rmaxx, rminy, DBL_MAX, rmaxy}};
+    for (int k = 0; k < 4; ++k)
+        for (int q = 0; q < 4; ++q) rm.comp[k][q] = (float)comp[k][q];
+
+    out.obj.resize(n);
+    float denom = 0;
+    for (int i = 0; i < n; ++i) {
+        mh::ObjConst& o = out.obj[i];
+        o.off = make_shape(vertices + offlimits[i].point1Index);
+        o.area = (float)(cfg[i].length * cfg[i].width);
+        o.frozen = cfg[i].frozen ? 1 : 0;
+        denom = denom + o.area;  // Kernel.cu:202, same order
+    }
+    rm.denom = denom;
+    out.clr.resize(c > 0 ? c : 1);
+    for (int i = 0; i < c; ++i) {
+        out.clr[i].shape = make_shape(vertices + clearances[i].point1Index);
+        out.clr[i].src = clearances[i].SourceIndex;
+    }
+    out.rel.resize(nr > 0 ? nr : 1);
+    for (int i = 0; i < nr; ++i) {
+        mh::RelConst& r = out.rel[i];
+        r.start = rss[i].TargetRange.targetRangeStart;
+        r.end = rss[i].TargetRange.targetRangeEnd;
+        r.s = rss[i].SourceIndex;
+        r.t = rss[i].TargetIndex;
+        r.amin = rsa[i].angleMin;
+        r.amax = rsa[i].angleMax;
+        r.as = rsa[i].SourceIndex;
+        r.at = rsa[i].TargetIndex;
+    }
+    out.cfg0.resize((size_t)mh::F_COUNT * n);
+    for (int i = 0; i < n; ++i) {
+        out.cfg0[mh::F_X * n + i] = cfg[i].x;
+        out.cfg0[mh::F_Y * n + i] = cfg[i].y;
+        out.cfg0[mh::F_Z * n + i] = cfg[i].z;
+        out.cfg0[mh::F_RX * n + i] = cfg[i].rotX;
+        out.cfg0[mh::F_RY * n + i] = cfg[i].rotY;
+        out.cfg0[mh::F_RZ * n + i] = cfg[i].rotZ;
+    }
+    return true;
+}
+
+struct Geometry {
+    int L, npl, waves;
+    mh::ChainLds lay;
+};
+
+bool choose_geometry(int n, int c, int device, Geometry& g) {
+    g.L = mh::choose_lanes(n);
+    g.npl = mh::choose_npl(n, g.L);
+    if (g.npl > mh::max_npl()) {
+        set_error("nObjs too large (max " + std::to_string(64 * mh::max_npl()) + ")");
+        return false;
+    }
+    g.lay = mh::make_lds_layout(n, c, g.L);
+    int max_lds = 0;
+    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
+        max_lds = 64 * 1024;
+    // Four waves per workgroup while that keeps at least two workgroups per CU.
+    g.waves = 4;
+    while (g.waves > 1 && mh::lds_bytes(g.lay, g.L, g.waves) > 80 * 1024) g.waves >>= 1;
+    if (mh::lds_bytes(g.lay, g.L, g.waves) > (size_t)max_lds) {
+        set_error("room does not fit in LDS");
+        return false;
+    }
+    return true;
+}
+
+uint64_t seed_from_env() {
+    const char* s = getenv("MH_SEED");
+    if (s && *s) return strtoull(s, nullptr, 0);
+    return (uint64_t)time(nullptr);  // Kernel.cu:943
+}
+
+}  // namespace
+
+struct mh_session {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Room room;
+    Geometry geo{};
+    int64_t n_chains = 0, chain_offset = 0;
+    uint64_t seed = 0;
+    mh::ObjConst* d_obj = nullptr;
+    mh::ClrConst* d_clr = nullptr;
+    mh::RelConst* d_rel = nullptr;
+    double* d_cfg0 = nullptr;
+    double* d_st = nullptr;
+    mh::ChainMeta* d_meta = nullptr;
+    point* d_pts = nullptr;
+    resultCosts* d_costs = nullptr;
+    mh_summary* d_summary = nullptr;
+
+    mh::LaunchArgs args() const {
+        mh::LaunchArgs a{};
+        a.rm = room.rm;
+        a.objc = d_obj;
+        a.clrc = d_clr;
+        a.relc = d_rel;
+        a.cfg = d_cfg0;
+        a.st = d_st;
+        a.meta = d_meta;
+        a.pts = d_pts;
+        a.costs = d_costs;
+        a.n_chains = n_chains;
+        a.chain_offset = chain_offset;
+        a.seed = seed;
+        a.iterations = 0;
+        a.lay = geo.lay;
+        return a;
+    }
+};
+
+namespace {
+
+void free_session(mh_session* s) {
+    if (!s) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    (void)hipFree(s->d_obj);
+    (void)hipFree(s->d_clr);
+    (void)hipFree(s->d_rel);
+    (void)hipFree(s->d_cfg0);
+    (void)hipFree(s->d_st);
+    (void)hipFree(s->d_meta);
+    (void)hipFree(s->d_pts);
+    (void)hipFree(s->d_costs);
+    (void)hipFree(s->d_summary);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    (void)hipSetDevice(prev);
+    delete s;
+}
+
+template <class T>
+bool upload(T** dst, const std::vector<T>& src, hipStream_t st) {
+    MH_TRY_HIP(hipMalloc((void**)dst, sizeof(T) * src.size()));
+    MH_TRY_HIP(hipMemcpyAsync(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice, st));
+    return true;
+}
+
+bool session_init(mh_session* s) {
+    MH_TRY_HIP(hipSetDevice(s->device));
+    MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->device, s->geo)) return false;
+    if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
+    if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
+    if (!upload(&s->d_rel, s->room.rel, s->stream)) return false;
+    if (!upload(&s->d_cfg0, s->room.cfg0, s->stream)) return false;
+    const int64_t nc = s->n_chains > 0 ? s->n_chains : 1;
+    const size_t n = (size_t)s->room.rm.n;
+    MH_TRY_HIP(hipMalloc((void**)&s->d_st, sizeof(double) * mh::F_COUNT * n * nc));
+    MH_TRY_HIP(hipMalloc((void**)&s->d_meta, sizeof(mh::ChainMeta) * nc));
+    MH_TRY_HIP(hipMalloc((void**)&s->d_pts, sizeof(point) * n * nc));
+    MH_TRY_HIP(hipMalloc((void**)&s->d_costs, sizeof(resultCosts) * nc));
+    MH_TRY_HIP(hipMalloc((void**)&s->d_summary, sizeof(mh_summary)));
+    MH_TRY_HIP(mh::launch(mh::OP_INIT, s->args(), s->geo.L, s->geo.npl, s->geo.waves, s->stream));
+    return true;
+}
+
+hipStream_t pick_stream(const mh_session* s, void* stream) {
+    return stream ? (hipStream_t)stream : s->stream;
+}
+
+bool session_run(mh_session* s, int iterations, hipStream_t st) {
+    MH_TRY_HIP(hipSetDevice(s->device));
+    if (st != s->stream) {
+        // Order the session's own setup work before work on a caller stream.
+        hipEvent_t ev;
+        MH_TRY_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        MH_TRY_HIP(hipEventRecord(ev, s->stream));
+        MH_TRY_HIP(hipStreamWaitEvent(st, ev, 0));
+        MH_TRY_HIP(hipEventDestroy(ev));
+    }
+    mh::LaunchArgs a = s->args();
+    for (int done = 0; done < iterations; done += kStepsPerLaunch) {
+        a.iterations = std::min(kStepsPerLaunch, iterations - done);
+        MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
+    }
+    return true;
+}
+
+bool session_finalize(mh_session* s, hipStream_t st) {
+    MH_TRY_HIP(hipSetDevice(s->device));
+    MH_TRY_HIP(mh::launch(mh::OP_FINAL, s->args(), s->geo.L, s->geo.npl, s->geo.waves, st));
+    return true;
+}
+
+bool session_download(mh_session* s, point* pts, resultCosts* costs) {
+    MH_TRY_HIP(hipSetDevice(s->device));
+    MH_TRY_HIP(hipDeviceSynchronize());
+    const size_t n = (size_t)s->room.rm.n;
+    if (pts && s->n_chains > 0)
+        MH_TRY_HIP(hipMemcpy(pts, s->d_pts, sizeof(point) * n * s->n_chains, hipMemcpyDeviceToHost));
+    if (costs && s->n_chains > 0)
+        MH_TRY_HIP(hipMemcpy(costs, s->d_costs, sizeof(resultCosts) * s->n_chains, hipMemcpyDeviceToHost));
+    return true;
+}
+
+mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
+                           uint64_t seed) {
+    mh_session* s = new mh_session();
+    s->device = device;
+    s->room = room;
+    s->n_chains = n_chains;
+    s->chain_offset = chain_offset;
+    s->seed = seed;
+    if (!session_init(s)) {
+        std::string e = g_last_error;
+        free_session(s);
+        set_error(e);
+        return nullptr;
+    }
+    return s;
+}
+
+std::vector<int> devices_from_env(int current) {
+    std::vector<int> d;
+    const char* s = getenv("MH_DEVICES");
+    if (!s || !*s) {
+        d.push_back(current);
+        return d;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    if (strcmp(s, "all") == 0) {
+        for (int i = 0; i < count; ++i) d.push_back(i);
+    } else {
+        std::string str(s);
+        size_t pos = 0;
+        while (pos <= str.size()) {
+            size_t e = str.find(',', pos);
+            if (e == std::string::npos) e = str.size();
+            if (e > pos) {
+                int v = atoi(str.substr(pos, e - pos).c_str());
+                if (v >= 0 && v < count) d.push_back(v);
+            }
+            pos = e + 1;
+        }
+    }
+    if (d.empty()) d.push_back(current);
+    return d;
+}
+
+// One device's share of a KernelWrapper call, run on its own host thread.
+struct Shard {
+    int device;
+    int64_t begin, count;
+    bool ok = false;
+    std::string err;
+};
+
+result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, positionAndRotation* cfg,
+                     rectangle* clearances, rectangle* offlimits, vertex* vertices,
+                     vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg, uint64_t seed) {
+    if (!gpuCfg) { set_error("gpuCfg is NULL"); return nullptr; }
+    if (gpuCfg->gridxDim < 1) { set_error("gpuConfig.gridxDim must be >= 1"); return nullptr; }
+    if (gpuCfg->iterations < 0) { set_error("gpuConfig.iterations must be >= 0"); return nullptr; }
+    Room room;
+    if (!build_room(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf, room))
+        return nullptr;
+    int current = 0;
+    if (hipGetDevice(&current) != hipSuccess) {
+        set_error("no HIP device available");
+        return nullptr;
+    }
+    const int64_t chains = gpuCfg->gridxDim;
+    const int iterations = gpuCfg->iterations;
+    const size_t n = (size_t)srf->nObjs;
+    std::vector<int> devs = devices_from_env(current);
+    if ((int64_t)devs.size() > chains) devs.resize((size_t)chains);
+
+    point* pts = (point*)malloc(sizeof(point) * n * (size_t)chains);
+    result* res = (result*)malloc(sizeof(result) * (size_t)chains);
+    std::vector<resultCosts> costs((size_t)chains);
+    if (!pts || !res) {
+        free(pts);
+        free(res);
+        set_error("host allocation failed");
+        return nullptr;
+    }
+    std::vector<Shard> shards(devs.size());
+    for (size_t k = 0; k < devs.size(); ++k) {
+        shards[k].device = devs[k];
+        shards[k].begin = chains * (int64_t)k / (int64_t)devs.size();
+        shards[k].count = chains * (int64_t)(k + 1) / (int64_t)devs.size() - shards[k].begin;
+    }
+    auto work = [&](Shard& sh) {
+        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed);
+        if (!s) {
+            sh.err = g_last_error;
+            return;
+        }
+        sh.ok = session_run(s, iterations, s->stream) && session_finalize(s, s->stream) &&
+                session_download(s, pts + n * sh.begin, costs.data() + sh.begin);
+        if (!sh.ok) sh.err = g_last_error;
+        free_session(s);
+    };
+    if (shards.size() == 1) {
+        work(shards[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (auto& sh : shards) th.emplace_back(work, std::ref(sh));
+        for (auto& t : th) t.join();
+    }
+    (void)hipSetDevice(current);
+    for (auto& sh : shards) {
+        if (!sh.ok) {
+            free(pts);
+            free(res);
+            set_error("device " + std::to_string(sh.device) + ": " + sh.err);
+            return nullptr;
+        }
+    }
+    for (int64_t i = 0; i < chains; ++i) {
+        res[i].points = pts + n * (size_t)i;
+        res[i].costs = costs[(size_t)i];
+    }
+    g_last_error.clear();
+    return res;
+}
+
+}  // namespace
+
+extern "C" {
+
+MH_API result* KernelWrapper(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                             positionAndRotation* cfg, rectangle* clearances, rectangle* offlimits,
+                             vertex* vertices, vertex* surfaceRectangle, Surface* srf,
+                             gpuConfig* gpuCfg) {
+    return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
+                        gpuCfg, seed_from_env());
+}
+
+MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                                   positionAndRotation* cfg, rectangle* clearances,
+                                   rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
+                                   Surface* srf, gpuConfig* gpuCfg, uint64_t seed) {
+    return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
+                        gpuCfg, seed);
+}
+
+MH_API void KernelFreeResult(result* res) {
+    if (!res) return;
+    free(res[0].points);
+    free(res);
+}
+
+MH_API const char* KernelLastError(void) { return g_last_error.c_str(); }
+
+MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationshipAngleStruct* rsa,
+                               const positionAndRotation* cfgs, int n_cfgs,
+                               const rectangle* clearances, const rectangle* offlimits,
+                               const vertex* vertices, const vertex* surfaceRectangle,
+                               const Surface* srf, resultCosts* out_costs) {
+    if (n_cfgs < 0 || !out_costs || !cfgs) { set_error("bad arguments"); return -1; }
+    Room room;
+    if (!build_room(rss, rsa, cfgs, clearances, offlimits, vertices, surfaceRectangle, srf, room))
+        return -1;
+    if (n_cfgs == 0) return 0;
+    const int n = srf->nObjs;
+    std::vector<double> all((size_t)n_cfgs * mh::F_COUNT * n);
+    for (int k = 0; k < n_cfgs; ++k) {
+        const positionAndRotation* c = cfgs + (size_t)k * n;
+        double* d = all.data() + (size_t)k * mh::F_COUNT * n;
+        for (int i = 0; i < n; ++i) {
+            d[mh::F_X * n + i] = c[i].x;
+            d[mh::F_Y * n + i] = c[i].y;
+            d[mh::F_Z * n + i] = c[i].z;
+            d[mh::F_RX * n + i] = c[i].rotX;
+            d[mh::F_RY * n + i] = c[i].rotY;
+            d[mh::F_RZ * n + i] = c[i].rotZ;
+        }
+    }
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) { set_error("no HIP device available"); return -1; }
+    mh_session* s = session_create(room, device, 0, 0, 0);  // tables only
+    if (!s) return -1;
+    bool ok = true;
+    double* d_cfgs = nullptr;
+    resultCosts* d_out = nullptr;
+    auto fail = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && ok) {
+            set_error(std::string(what) + ": " + hipGetErrorString(e));
+            ok = false;
+        }
+    };
+    fail(hipMalloc((void**)&d_cfgs, sizeof(double) * all.size()), "hipMalloc");
+    if (ok) fail(hipMalloc((void**)&d_out, sizeof(resultCosts) * n_cfgs), "hipMalloc");
+    if (ok) fail(hipMemcpy(d_cfgs, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    if (ok) {
+        mh::LaunchArgs a = s->args();
+        a.cfg = d_cfgs;
+        a.costs = d_out;
+        a.n_chains = n_cfgs;
+        fail(mh::launch(mh::OP_EVAL, a, s->geo.L, s->geo.npl, s->geo.waves, s->stream), "launch");
+    }
+    if (ok) fail(hipStreamSynchronize(s->stream), "hipStreamSynchronize");
+    if (ok) fail(hipMemcpy(out_costs, d_out, sizeof(resultCosts) * n_cfgs, hipMemcpyDeviceToHost), "hipMemcpy");
+    (void)hipFree(d_cfgs);
+    (void)hipFree(d_out);
+    free_session(s);
+    return ok ? 0 : -1;
+}
+
+MH_API mh_session* mh_session_create(const relationshipStruct* rss,
+                                     const relationshipAngleStruct* rsa,
+                                     const positionAndRotation* cfg, const rectangle* clearances,
+                                     const rectangle* offlimits, const vertex* vertices,
+                                     const vertex* surfaceRectangle, const Surface* srf,
+                                     int device, int64_t n_chains, int64_t chain_offset,
+                                     uint64_t seed) {
+    if (n_chains < 0 || chain_offset < 0) { set_error("negative chain count or offset"); return nullptr; }
+    Room room;
+    if (!build_room(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf, room))
+        return nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) {
+        set_error("invalid HIP device " + std::to_string(device));
+        return nullptr;
+    }
+    return session_create(room, device, n_chains, chain_offset, seed);
+}
+
+MH_API int mh_session_run(mh_session* s, int iterations, void* stream) {
+    if (!s || iterations < 0) { set_error("bad arguments"); return -1; }
+    return session_run(s, iterations, pick_stream(s, stream)) ? 0 : -1;
+}
+
+MH_API int mh_session_finalize(mh_session* s, void* stream) {
+    if (!s) { set_error("NULL session"); return -1; }
+    return session_finalize(s, pick_stream(s, stream)) ? 0 : -1;
+}
+
+MH_API int mh_session_download(mh_session* s, point* out_points, resultCosts* out_costs) {
+    if (!s) { set_error("NULL session"); return -1; }
+    return session_download(s, out_points, out_costs) ? 0 : -1;
+}
+
+MH_API int mh_session_summary(mh_session* s, mh_summary* out) {
+    if (!s || !out) { set_error("bad arguments"); return -1; }
+    if (hipSetDevice(s->device) != hipSuccess) { set_error("hipSetDevice failed"); return -1; }
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = mh::launch_summary(s->d_costs, s->d_meta, s->n_chains, s->chain_offset, s->d_summary, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, s->d_summary, sizeof(mh_summary), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        set_error(std::string("summary: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* chains_per_workgroup) {
+    if (!s) { set_error("NULL session"); return -1; }
+    if (lanes_per_chain) *lanes_per_chain = s->geo.L;
+    if (chains_per_workgroup) *chains_per_workgroup = s->geo.waves * (64 / s->geo.L);
+    return 0;
+}
+
+MH_API void mh_session_destroy(mh_session* s) { free_session(s); }
+
+// Diagnostic: the Philox words, uniforms and normals a chain with this (seed, subsequence)
+// draws, exactly as the chain kernel draws them. Returns 0 on success.
+MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
+                        float* out_uniform, float* out_normal) {
+    if (n < 0 || !out_u32 || !out_uniform || !out_normal) { set_error("bad arguments"); return -1; }
+    if (n == 0) return 0;
+    unsigned int* d_u = nullptr;
+    float *d_f = nullptr, *d_n = nullptr;
+    hipError_t e = hipMalloc((void**)&d_u, sizeof(unsigned int) * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_f, sizeof(float) * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_n, sizeof(float) * n);
+    if (e == hipSuccess) e = mh::launch_rng(seed, subsequence, n, d_u, d_f, d_n, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out_u32, d_u, sizeof(unsigned int) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_uniform, d_f, sizeof(float) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_normal, d_n, sizeof(float) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_u);
+    (void)hipFree(d_f);
+    (void)hipFree(d_n);
+    if (e != hipSuccess) {
+        set_error(std::string("mh_debug_rng: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"

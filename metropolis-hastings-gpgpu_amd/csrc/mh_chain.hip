@@ -1,0 +1,826 @@
+// mh_chain.hip -- MI355X (gfx950) Metropolis-Hastings interior-layout chains.
+//
+// Rebuilds the reference's per-chain hot path (KernelFolder/Kernel/Kernel.cu:754-871: propose
+// :576-704, Costs :516-550, Accept :706-713) for CDNA4:
+//   * a chain is a group of L lanes (L = 64 -> one wavefront per chain; L = 8..32 for small
+//     rooms, 64/L chains per wavefront); each lane owns objects r, r+L, r+2L, ...;
+//   * the chain's configuration lives in LDS for the whole launch; the proposal edits at most
+//     two objects IN PLACE and a rejected proposal is undone from a register backup (the
+//     reference copies the whole configuration twice per step, Kernel.cu:792,824);
+//   * the O(N^2) symmetry rows and the O(C*N) clearance pairs are spread over the lanes; the
+//     reference's float/double sums are replayed serially in the reference's order through
+//     readlane/ds_bpermute (so results are bit-identical, not merely close), skipping exact
+//     zeros (x - 0 == x);
+//   * OffLimitsCosts never enters totalCosts (Kernel.cu:547) and so cannot change a decision:
+//     it is evaluated once, for the final state only;
+//   * the RNG is rocRAND's Philox4x32-10 (seed, subsequence = global chain id), resumable by
+//     draw count, so k launches of m steps equal one launch of k*m steps.
+// Compiled with -ffp-contract=off: every multiply and add rounds where the reference's does.
+
+#include <hip/hip_runtime.h>
+#include <rocrand/rocrand_philox4x32_10.h>
+#include <rocrand/rocrand_uniform.h>
+
+#include <stdint.h>
+
+#include "mh_launch.h"
+
+namespace mh {
+
+struct ObjP {  // per-object pose words read by the O(N^2) symmetry loop: one ds_read_b128
+    float xf, yf;  // (float)x, (float)y -- every O(N^2) use of x, y is through float args
+    double rotY;
+};
+
+struct Backup {
+    int k;
+    double x, y, z, rx, ry, rz;
+};
+
+// Per-chain scalars kept in LDS rather than registers while the costs are evaluated.
+struct ChainAux {
+    Backup b[2];
+    int nb;       // backups in use (0, 1 or 2)
+    float cur[8]; // resultCosts of the current configuration
+};
+static_assert(sizeof(ChainAux) <= 192, "ChainAux");
+
+struct ChainPtrs {
+    ObjP* P;
+    double *X, *Y, *Z, *RX, *RZ;
+    float4* OFF;
+    float4* CLA;
+    ChainAux* aux;
+};
+
+// ---- wave-level helpers -----------------------------------------------------------------
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int L>
+__device__ __forceinline__ uint64_t group_ballot(bool pred, int gbase) {
+    uint64_t b = __ballot(pred);
+    if constexpr (L == 64) {
+        return b;
+    } else {
+        return (b >> gbase) & ((1ull << L) - 1ull);
+    }
+}
+
+// Value of v held by lane `src` of this lane's group (src is group-uniform).
+template <int L>
+__device__ __forceinline__ float grp_get(float v, int src, int gbase) {
+    if constexpr (L == 64) {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+    } else {
+        return __int_as_float(__builtin_amdgcn_ds_bpermute((gbase + src) << 2, __float_as_int(v)));
+    }
+}
+
+template <int L>
+__device__ __forceinline__ double grp_get(double v, int src, int gbase) {
+    int2 w = *reinterpret_cast<int2*>(&v);
+    int2 o;
+    if constexpr (L == 64) {
+        o.x = __builtin_amdgcn_readlane(w.x, src);
+        o.y = __builtin_amdgcn_readlane(w.y, src);
+    } else {
+        o.x = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.x);
+        o.y = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.y);
+    }
+    return *reinterpret_cast<double*>(&o);
+}
+
+// ---- RNG ----------------------------------------------------------------------------------
+
+// Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
+// OCML log/sin/cos code is not duplicated at every call site.
+__device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
+    const double u1 = (double)a * 0x1p-32 + 0x1p-33;
+    const double u2 = (double)b * 0x1p-32 + 0x1p-33;
+    const double rad = sqrt(-2.0 * log(u1));
+    const double ang = 6.283185307179586 * u2;
+    return make_float2((float)(rad * sin(ang)), (float)(rad * cos(ang)));
+}
+
+// rocRAND Philox4x32-10 stream of one chain. Words are taken a block of four at a time with
+// rocrand4() (identical to four rocrand() calls from substate 0) and selected without dynamic
+// register indexing, so the state stays in registers.
+struct ChainRng {
+    rocrand_state_philox4x32_10 st;
+    uint4 buf;          // current block
+    int idx;            // next word of buf (4 = exhausted)
+    uint64_t draws;     // words consumed since draw 0
+    int bm_has;
+    float bm_val;
+
+    __device__ __forceinline__ void init(uint64_t seed, uint64_t subsequence, uint64_t offset) {
+        rocrand_init(seed, subsequence, offset & ~3ull, &st);
+        buf = rocrand4(&st);
+        idx = (int)(offset & 3);
+        draws = offset;
+    }
+    __device__ __forceinline__ unsigned int next() {
+        if (idx == 4) {
+            buf = rocrand4(&st);
+            idx = 0;
+        }
+        const unsigned int v = idx == 0 ? buf.x : idx == 1 ? buf.y : idx == 2 ? buf.z : buf.w;
+        ++idx;
+        ++draws;
+        return v;
+    }
+    // curand_uniform stand-in (Kernel.cu:569,710): rocRAND's (0,1] float conversion.
+    __device__ __forceinline__ float uniform() {
+        return rocrand_device::detail::uniform_distribution(next());
+    }
+    // curand_normal stand-in (Kernel.cu:605,608,641): sine branch first, cosine branch cached
+    // for the next call (cuRAND's caching order).
+    __device__ __forceinline__ float normal() {
+        if (bm_has) {
+            bm_has = 0;
+            return bm_val;
+        }
+        const unsigned int a = next();
+        const unsigned int b = next();
+        const float2 z = box_muller(a, b);
+        bm_val = z.y;
+        bm_has = 1;
+        return z.x;
+    }
+};
+
+// ---- numerics shared by every term ---------------------------------------------------------
+
+// Kernel.cu:162-167: float difference, double root.
+__device__ __forceinline__ double distance_f(float xi, float yi, float xj, float yj) {
+    float fx = xi - xj;
+    float fy = yi - yj;
+    double dx = fx, dy = fy;
+    double sq = dx * dx;
+    sq = sq + dy * dy;
+    return sqrt(sq);
+}
+
+// Kernel.cu:170-182.
+__device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {
+    double dx = (double)(float)(xi - xj);
+    double dy = (double)(float)(yi - yj);
+    double tp = atan2(dy, dx);
+    if (tp < 0) tp = kTwoPI + tp;
+    double t = tp - (double)ti;
+    return (t < 0) ? kTwoPI + t : t;
+}
+
+// The reference's float atan2f / cosf, evaluated as the double function rounded once.
+__device__ __forceinline__ float atan2_f32(float y, float x) {
+    return (float)atan2((double)y, (double)x);
+}
+__device__ __forceinline__ float cos_f32(float x) { return (float)cos((double)x); }
+
+// minValue/maxValue (Kernel.cu:366-401) of a rectangle translated by (tx, ty), as floats.
+__device__ __forceinline__ float4 shape_box(const RectShape& s, float tx, float ty) {
+    float4 b;
+    b.x = fminf(s.v0x, (float)(s.xmin1 + (double)tx));
+    b.y = (float)(s.ymin + (double)ty);
+    b.z = (float)(s.xmax + (double)tx);
+    b.w = (float)(s.ymax + (double)ty);
+    return b;
+}
+
+// calculateIntersectionArea, Kernel.cu:321-340 (boxes already rounded to float).
+__device__ __forceinline__ float overlap(float4 a, float4 b) {
+    float x5 = fmaxf(a.x, b.x);
+    float y5 = fmaxf(a.y, b.y);
+    float x6 = fminf(a.z, b.z);
+    float y6 = fminf(a.w, b.w);
+    if (x5 >= x6 || y5 >= y6) return 0.0f;
+    return (x6 - x5) * (y6 - y5);
+}
+
+__device__ __forceinline__ float4 comp_overlaps(const DevRoom& rm, float4 box) {
+    float4 t;
+    t.x = overlap(box, make_float4(rm.comp[0][0], rm.comp[0][1], rm.comp[0][2], rm.comp[0][3]));
+    t.y = overlap(box, make_float4(rm.comp[1][0], rm.comp[1][1], rm.comp[1][2], rm.comp[1][3]));
+    t.z = overlap(box, make_float4(rm.comp[2][0], rm.comp[2][1], rm.comp[2][2], rm.comp[2][3]));
+    t.w = overlap(box, make_float4(rm.comp[3][0], rm.comp[3][1], rm.comp[3][2], rm.comp[3][3]));
+    return t;
+}
+
+__device__ __forceinline__ bool nonzero4(float4 t) {
+    return t.x != 0.0f || t.y != 0.0f || t.z != 0.0f || t.w != 0.0f;
+}
+
+// Serially subtract, in lane order, the float4 terms of the group's lanes that are non-zero.
+template <int L>
+__device__ __forceinline__ float serial_sub4(float acc, float4 t, int gbase) {
+    uint64_t bits = group_ballot<L>(nonzero4(t), gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t.x, b, gbase);
+        acc = acc - grp_get<L>(t.y, b, gbase);
+        acc = acc - grp_get<L>(t.z, b, gbase);
+        acc = acc - grp_get<L>(t.w, b, gbase);
+    }
+    return acc;
+}
+
+template <int L>
+__device__ __forceinline__ float serial_sub(float acc, float t, int gbase) {
+    uint64_t bits = group_ballot<L>(t != 0.0f, gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t, b, gbase);
+    }
+    return acc;
+}
+
+template <int L>
+__device__ __forceinline__ double serial_sub(double acc, double t, int gbase) {
+    uint64_t bits = group_ballot<L>(t != 0.0, gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t, b, gbase);
+    }
+    return acc;
+}
+
+// ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
+//
+// Every lane of the group returns the same costs. out: resultCosts order
+// {total, PW, VB, FP, SYM, CL, OL, SA}.
+template <int L, int NPL, bool WITH_OL>
+__device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
+                           float out[8]) {
+    const DevRoom& rm = a.rm;
+    const int n = rm.n, c = rm.c;
+
+    // Phase A: per-object and per-clearance terms of the owned slots.
+    double px[NPL], py[NPL];
+    float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
+    float4 sao[NPL], sac[NPL];
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        px[m] = py[m] = 0.0;
+        cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
+        sao[m] = sac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < n) {
+            const ObjConst oc = a.objc[i];
+            const ObjP p = ch.P[i];
+            const double x = ch.X[i], y = ch.Y[i];
+            // VisualBalanceCosts products, Kernel.cu:200-201.
+            px[m] = (double)oc.area * x;
+            py[m] = (double)oc.area * y;
+            // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188.
+            float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
+            float b = at - (float)p.rotY;
+            float ph = (float)((double)b + kHalfPI);
+            cph[m] = cos_f32(ph);
+            // SymmetryCosts row setup, Kernel.cu:292-299.
+            double al = x * (double)rm.ux;
+            al = al + y * (double)rm.uy;
+            float sd = (float)(2.0 * (rm.along_f - al));
+            rxs[m] = (float)(x + (double)(sd * rm.ux));
+            rys[m] = (float)(y + (double)(sd * rm.uy));
+            float rr = (float)(rm.two_focal_rot - p.rotY);
+            if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
+            rrs[m] = rr;
+            // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
+            float4 box = shape_box(oc.off, p.xf, p.yf);
+            ch.OFF[i] = box;
+            sao[m] = comp_overlaps(rm, box);
+        }
+        if (i < c) {
+            const ClrConst cc = a.clrc[i];
+            const ObjP ps = ch.P[cc.src];
+            ch.CLA[i] = shape_box(cc.shape, ps.xf, ps.yf);       // ClearanceCosts, :414-415
+            const ObjP pi = ch.P[i];                              // SurfaceArea quirk: cfg[i], :456
+            sac[m] = comp_overlaps(rm, shape_box(cc.shape, pi.xf, pi.yf));
+        }
+    }
+    wave_sync();
+
+    // Phase B: symmetry rows, Kernel.cu:301-312 (max is exact, so any j order works).
+    float rowmax[NPL];
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        float best = 0.0f;
+        if (i < n) {
+            const float rx = rxs[m], ry = rys[m];
+            const double rr = (double)rrs[m];
+#pragma unroll 4
+            for (int j = 0; j < n; ++j) {
+                const ObjP q = ch.P[j];
+                float dp = (float)distance_f(q.xf, q.yf, rx, ry);
+                float dt = (float)(q.rotY - rr);
+                if (dt > kPI) dt = (float)((double)dt - kTwoPI);
+                float head = 5.0f - sqrtf(dp);
+                float val = (float)((double)head - 0.4 * (double)fabsf(dt));
+                best = fmaxf(best, val);
+            }
+        }
+        rowmax[m] = best;
+    }
+
+    // Phase C: the object-ordered sums (VisualBalance nx/ny, FocalPoint, Symmetry).
+    float nx = 0.0f, ny = 0.0f, sym = 0.0f;
+    double fp = 0.0;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int cnt = min(L, n - m * L);
+        for (int l = 0; l < cnt; ++l) {
+            nx = (float)((double)nx + grp_get<L>(px[m], l, gbase));
+            ny = (float)((double)ny + grp_get<L>(py[m], l, gbase));
+            fp = fp - (double)grp_get<L>(cph[m], l, gbase);
+            sym = sym - grp_get<L>(rowmax[m], l, gbase);
+        }
+    }
+    const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
+
+    // Phase D: SurfaceAreaCosts, clearances first then objects (Kernel.cu:453-480).
+    float sa = 0.0f;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m)
+        if (m * L < c) sa = serial_sub4<L>(sa, sac[m], gbase);
+#pragma unroll
+    for (int m = 0; m < NPL; ++m)
+        if (m * L < n) sa = serial_sub4<L>(sa, sao[m], gbase);
+
+    // Phase E: ClearanceCosts, clearance-major, object-minor (Kernel.cu:408-431).
+    float cl = 0.0f;
+    for (int ci = 0; ci < c; ++ci) {
+        const float4 A = ch.CLA[ci];
+        for (int jb = 0; jb < n; jb += L) {
+            const int j = jb + r;
+            const float ar = (j < n) ? overlap(A, ch.OFF[j]) : 0.0f;
+            cl = serial_sub<L>(cl, ar, gbase);
+        }
+    }
+
+    // Phase F: PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263).
+    double pw = 0.0, ang = 0.0;
+    for (int qb = 0; qb < rm.r; qb += L) {
+        const int q = qb + r;
+        double tpw = 0.0, tang = 0.0;
+        if (q < rm.r) {
+            const RelConst rc = a.relc[q];
+            const ObjP s0 = ch.P[rc.s], t0 = ch.P[rc.t];
+            const double d = distance_f(s0.xf, s0.yf, t0.xf, t0.yf);
+            if (d < rc.start) {
+                double f = d / rc.start;
+                tpw = f * f;
+            } else if (d > rc.end) {
+                double f = rc.end / d;
+                tpw = f * f;
+            }
+            const ObjP s1 = ch.P[rc.as], t1 = ch.P[rc.at];
+            const double th = theta_f(s1.xf, s1.yf, t1.xf, t1.yf, (float)t1.rotY);
+            if (rc.amin > rc.amax) {
+                double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
+                float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
+                if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+            } else if (rc.amin < th || th < rc.amax) {
+                double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
+                tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+            }
+        }
+        pw = serial_sub<L>(pw, tpw, gbase);
+        ang = serial_sub<L>(ang, tang, gbase);
+    }
+
+    // OffLimitsCosts, pairs i < j (Kernel.cu:488-511): final / evaluation passes only.
+    float ol = 0.0f;
+    if constexpr (WITH_OL) {
+        for (int i = 0; i < n; ++i) {
+            const float4 A = ch.OFF[i];
+            for (int jb = i + 1; jb < n; jb += L) {
+                const int j = jb + r;
+                const float ar = (j < n) ? overlap(A, ch.OFF[j]) : 0.0f;
+                ol = serial_sub<L>(ol, ar, gbase);
+            }
+        }
+    }
+
+    // Costs(), Kernel.cu:518-549.
+    const float pwc = (float)(pw * ang);
+    out[1] = rm.w_pw * pwc;
+    out[2] = rm.w_vb * vb;
+    out[3] = rm.w_fp * (float)fp;
+    out[4] = rm.w_sym * sym;
+    out[6] = rm.w_ol * ol;
+    out[5] = rm.w_cl * cl;
+    out[7] = rm.w_sa * sa;
+    float t = out[1] + out[2];
+    t = t + out[3];
+    t = t + out[4];
+    t = t + out[5];
+    t = t + out[7];
+    out[0] = t;
+}
+
+// ---- propose(), Kernel.cu:566-704, applied in place --------------------------------------
+
+__device__ __forceinline__ int rand_int(ChainRng& rng, int max, int min) {
+    float u = rng.uniform();
+    u = (float)((double)u * ((double)(max - min) + 0.999999));
+    u = u + (float)min;
+    return (int)truncf(u);
+}
+
+__device__ __forceinline__ int pick_object(ChainRng& rng, int n, const unsigned char* frozen) {
+    int k = rand_int(rng, n - 1, 0);
+    while (frozen[k]) k = rand_int(rng, n - 1, 0);  // frozen[n] == 1: index n is redrawn
+    return k;
+}
+
+__device__ __forceinline__ Backup read_obj(const ChainPtrs& ch, int k) {
+    Backup b;
+    b.k = k;
+    b.x = ch.X[k];
+    b.y = ch.Y[k];
+    b.z = ch.Z[k];
+    b.rx = ch.RX[k];
+    b.ry = ch.P[k].rotY;
+    b.rz = ch.RZ[k];
+    return b;
+}
+
+__device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, double y, double z,
+                                          double rx, double ry, double rz) {
+    ch.X[k] = x;
+    ch.Y[k] = y;
+    ch.Z[k] = z;
+    ch.RX[k] = rx;
+    ch.RZ[k] = rz;
+    ObjP p;
+    p.xf = (float)x;
+    p.yf = (float)y;
+    p.rotY = ry;
+    ch.P[k] = p;
+}
+
+// Applies one proposal to the configuration in LDS; `writer` also records the overwritten
+// objects in ch.aux so a rejection can undo them.
+__device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* frozen,
+                        const ChainPtrs& ch, bool writer) {
+    const int n = rm.n;
+    const int mode = rand_int(rng, 2, 0);
+    if (mode == 0) {  // translate, Kernel.cu:595-632
+        const int k = pick_object(rng, n, frozen);
+        float dx = rng.normal();
+        dx = dx * rm.sx;
+        float dy = rng.normal();
+        dy = dy * rm.sy;
+        const Backup b0 = read_obj(ch, k);
+        double x = b0.x, y = b0.y;
+        if (x + (double)dx > rm.rmax_x) x = rm.rmax_x;
+        else if (x + (double)dx < rm.rmin_x) x = rm.rmin_x;
+        else x = x + (double)dx;
+        if (y + (double)dy > rm.rmax_y) y = rm.rmax_y;
+        else if (y + (double)dy < rm.rmin_y) y = rm.rmin_y;
+        else y = y + (double)dy;
+        if (writer) {
+            ch.aux->b[0] = b0;
+            ch.aux->nb = 1;
+            write_obj(ch, k, x, y, b0.z, b0.rx, b0.ry, b0.rz);
+        }
+        return;
+    }
+    if (mode == 1) {  // rotate, Kernel.cu:634-653
+        const int k = pick_object(rng, n, frozen);
+        float dr = rng.normal();
+        dr = (float)((double)dr * kSigmaT);
+        const Backup b0 = read_obj(ch, k);
+        double ry = b0.ry + (double)dr;
+        if (ry < 0) ry = ry + kTwoPI;
+        else if (ry > kTwoPI) ry = ry - kTwoPI;
+        if (writer) {
+            ch.aux->b[0] = b0;
+            ch.aux->nb = 1;
+            write_obj(ch, k, b0.x, b0.y, b0.z, b0.rx, ry, b0.rz);
+        }
+        return;
+    }
+    // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
+    if (n < 2) {
+        if (writer) ch.aux->nb = 0;
+        return;
+    }
+    const int ka = pick_object(rng, n, frozen);
+    const int kb = pick_object(rng, n, frozen);
+    if (writer) {
+        const Backup b0 = read_obj(ch, ka);
+        const Backup b1 = read_obj(ch, kb);
+        ch.aux->b[0] = b0;
+        ch.aux->b[1] = b1;
+        ch.aux->nb = 2;
+        write_obj(ch, ka, b1.x, b1.y, b1.z, b1.rx, b1.ry, b1.rz);
+        write_obj(ch, kb, (double)(float)b0.x, (double)(float)b0.y, (double)(float)b0.z,
+                  (double)(float)b0.rx, (double)(float)b0.ry, (double)(float)b0.rz);
+    }
+}
+
+// Undo the last proposal (writer lane only).
+__device__ __forceinline__ void restore(const ChainPtrs& ch) {
+    const int nb = ch.aux->nb;
+    for (int q = nb - 1; q >= 0; --q) {
+        const Backup b = ch.aux->b[q];
+        write_obj(ch, b.k, b.x, b.y, b.z, b.rx, b.ry, b.rz);
+    }
+}
+
+// Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
+__device__ __forceinline__ bool accept(ChainRng& rng, float star, float cur) {
+    const float u = rng.uniform();
+    const float thr = fminf(1.0f, (float)exp(kBeta * ((double)star - (double)cur)));
+    return u < thr;
+}
+
+// ---- the kernel ---------------------------------------------------------------------------
+
+template <int L, int NPL, int OP>
+__global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int G = 64 / L;
+    const int n = a.rm.n;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = (L == 64) ? 0 : lane / L;
+    const int r = (L == 64) ? lane : lane % L;
+    const int gbase = g * L;
+    const int waves_per_wg = blockDim.x >> 6;
+
+    unsigned char* frozen = lds;
+    for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
+    __syncthreads();
+
+    const int64_t chain = ((int64_t)blockIdx.x * waves_per_wg + wave) * G + g;
+    if (chain >= a.n_chains) return;
+
+    unsigned char* base = lds + a.lay.hdr + (wave * G + g) * a.lay.stride;
+    ChainPtrs ch;
+    ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
+    ch.X = reinterpret_cast<double*>(base + a.lay.X);
+    ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
+    ch.Z = reinterpret_cast<double*>(base + a.lay.Z);
+    ch.RX = reinterpret_cast<double*>(base + a.lay.RX);
+    ch.RZ = reinterpret_cast<double*>(base + a.lay.RZ);
+    ch.OFF = reinterpret_cast<float4*>(base + a.lay.OFF);
+    ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
+    ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
+
+    // Stage the configuration into LDS.
+    const double* src;
+    if constexpr (OP == OP_INIT) src = a.cfg;
+    else if constexpr (OP == OP_EVAL) src = a.cfg + chain * (int64_t)(F_COUNT * n);
+    else src = a.st + chain * (int64_t)(F_COUNT * n);
+    for (int i = r; i < n; i += L) {
+        const double x = src[F_X * n + i], y = src[F_Y * n + i];
+        ch.X[i] = x;
+        ch.Y[i] = y;
+        ch.Z[i] = src[F_Z * n + i];
+        ch.RX[i] = src[F_RX * n + i];
+        ch.RZ[i] = src[F_RZ * n + i];
+        ObjP p;
+        p.xf = (float)x;
+        p.yf = (float)y;
+        p.rotY = src[F_RY * n + i];
+        ch.P[i] = p;
+    }
+    wave_sync();
+
+    float cur[8];
+    if constexpr (OP == OP_INIT) {
+        eval_costs<L, NPL, false>(a, ch, r, gbase, cur);
+        if (r == 0) {
+            ChainMeta m;
+            m.draws = 0;
+            m.accepted = 0;
+            m.bm_has = 0;
+            m.bm_val = 0.0f;
+            for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
+            m.pad[0] = m.pad[1] = 0;
+            a.meta[chain] = m;
+        }
+    } else if constexpr (OP == OP_STEP) {
+        const ChainMeta m0 = a.meta[chain];
+        const bool writer = (r == 0);
+        if (writer)
+            for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
+        float cur_total = m0.costs[0];
+        ChainRng rng;
+        rng.init(a.seed, (uint64_t)(a.chain_offset + chain), m0.draws);
+        rng.bm_has = m0.bm_has;
+        rng.bm_val = m0.bm_val;
+        uint64_t accepted = m0.accepted;
+        for (int it = 0; it < a.iterations; ++it) {
+            propose(rng, a.rm, frozen, ch, writer);
+            wave_sync();
+            float sc[8];
+            eval_costs<L, NPL, false>(a, ch, r, gbase, sc);
+            if (accept(rng, sc[0], cur_total)) {
+                cur_total = sc[0];
+                ++accepted;
+                if (writer)
+                    for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
+            } else if (writer) {
+                restore(ch);
+            }
+            wave_sync();
+        }
+        if (writer) {
+            ChainMeta m;
+            m.draws = rng.draws;
+            m.accepted = accepted;
+            m.bm_has = rng.bm_has;
+            m.bm_val = rng.bm_val;
+            for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
+            m.pad[0] = m.pad[1] = 0;
+            a.meta[chain] = m;
+        }
+    } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
+        eval_costs<L, NPL, true>(a, ch, r, gbase, cur);
+        if (r == 0) {
+            resultCosts rc;
+            rc.totalCosts = cur[0];
+            rc.PairWiseCosts = cur[1];
+            rc.VisualBalanceCosts = cur[2];
+            rc.FocalPointCosts = cur[3];
+            rc.SymmetryCosts = cur[4];
+            rc.ClearanceCosts = cur[5];
+            rc.OffLimitsCosts = cur[6];
+            rc.SurfaceAreaCosts = cur[7];
+            a.costs[chain] = rc;
+        }
+        if constexpr (OP == OP_FINAL) {
+            for (int i = r; i < n; i += L) {
+                point p;
+                p.x = (float)ch.X[i];
+                p.y = (float)ch.Y[i];
+                p.z = (float)ch.Z[i];
+                p.rotX = (float)ch.RX[i];
+                p.rotY = (float)ch.P[i].rotY;
+                p.rotZ = (float)ch.RZ[i];
+                a.pts[chain * (int64_t)n + i] = p;
+            }
+        }
+    }
+
+    if constexpr (OP == OP_INIT || OP == OP_STEP) {
+        double* dst = a.st + chain * (int64_t)(F_COUNT * n);
+        for (int i = r; i < n; i += L) {
+            dst[F_X * n + i] = ch.X[i];
+            dst[F_Y * n + i] = ch.Y[i];
+            dst[F_Z * n + i] = ch.Z[i];
+            dst[F_RX * n + i] = ch.RX[i];
+            dst[F_RY * n + i] = ch.P[i].rotY;
+            dst[F_RZ * n + i] = ch.RZ[i];
+        }
+    }
+}
+
+// ---- summary reduction (for the multi-GPU best-cost all-gather) ---------------------------
+
+__global__ void __launch_bounds__(1024) mh_summary_kernel(const resultCosts* costs,
+                                                          const ChainMeta* meta, int64_t n,
+                                                          int64_t chain_offset, mh_summary* out) {
+    __shared__ double s_sum[1024];
+    __shared__ float s_best[1024];
+    __shared__ int64_t s_arg[1024];
+    __shared__ int64_t s_acc[1024];
+    double sum = 0.0;
+    float best = -INFINITY;
+    int64_t arg = -1, acc = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float t = costs[i].totalCosts;
+        sum += (double)t;
+        if (t > best || arg < 0) {
+            best = t;
+            arg = i;
+        }
+        acc += (int64_t)meta[i].accepted;
+    }
+    s_sum[threadIdx.x] = sum;
+    s_best[threadIdx.x] = best;
+    s_arg[threadIdx.x] = arg;
+    s_acc[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            const int o = threadIdx.x + w;
+            s_sum[threadIdx.x] += s_sum[o];
+            s_acc[threadIdx.x] += s_acc[o];
+            const bool take = s_arg[o] >= 0 &&
+                              (s_arg[threadIdx.x] < 0 || s_best[o] > s_best[threadIdx.x] ||
+                               (s_best[o] == s_best[threadIdx.x] && s_arg[o] < s_arg[threadIdx.x]));
+            if (take) {
+                s_best[threadIdx.x] = s_best[o];
+                s_arg[threadIdx.x] = s_arg[o];
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        mh_summary s;
+        s.sum_total = s_sum[0];
+        s.best_total = s_best[0];
+        s.pad = 0;
+        s.best_chain = s_arg[0] < 0 ? -1 : s_arg[0] + chain_offset;
+        s.n_chains = n;
+        s.accepted = s_acc[0];
+        *out = s;
+    }
+}
+
+// ---- RNG diagnostic: the exact draws a chain sees --------------------------------------
+
+__global__ void mh_rng_kernel(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
+                              float* uni, float* nrm) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ChainRng r;
+    r.bm_has = 0;
+    r.bm_val = 0.f;
+    r.init(seed, subsequence, 0);
+    for (int i = 0; i < n; ++i) u32[i] = r.next();
+    r.init(seed, subsequence, 0);
+    for (int i = 0; i < n; ++i) uni[i] = r.uniform();
+    r.init(seed, subsequence, 0);
+    for (int i = 0; i < n; ++i) nrm[i] = r.normal();
+}
+
+// ---- host-side launch dispatch ------------------------------------------------------------
+
+template <int L, int NPL>
+static hipError_t launch_geom(int op, const LaunchArgs& a, int waves_per_wg, hipStream_t stream) {
+    constexpr int G = 64 / L;
+    const int64_t chains_per_wg = (int64_t)waves_per_wg * G;
+    const int64_t blocks = (a.n_chains + chains_per_wg - 1) / chains_per_wg;
+    const size_t lds = (size_t)a.lay.hdr + (size_t)waves_per_wg * G * a.lay.stride;
+    const dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_wg));
+    switch (op) {
+        case OP_INIT: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_INIT>), grid, block, lds, stream, a); break;
+        case OP_STEP: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_STEP>), grid, block, lds, stream, a); break;
+        case OP_FINAL: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_FINAL>), grid, block, lds, stream, a); break;
+        default: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_EVAL>), grid, block, lds, stream, a); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mh
+
+// Entry points used by mh_abi.cpp.
+namespace mh {
+
+// Lanes per chain: the next power of two >= N (at least 8, at most 64); objects per lane
+// (NPL) covers N > 64.
+int choose_lanes(int n) {
+    int L = 8;
+    while (L < n && L < 64) L <<= 1;
+    return L;
+}
+int choose_npl(int n, int L) { return (n + L - 1) / L; }
+int max_npl() { return 8; }
+
+size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
+    return (size_t)lay.hdr + (size_t)waves_per_wg * (64 / L) * lay.stride;
+}
+
+hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
+    if (a.n_chains <= 0) return hipSuccess;
+    switch (L) {
+        case 8: return launch_geom<8, 1>(op, a, waves_per_wg, s);
+        case 16: return launch_geom<16, 1>(op, a, waves_per_wg, s);
+        case 32: return launch_geom<32, 1>(op, a, waves_per_wg, s);
+        default: break;
+    }
+    switch (npl) {
+        case 1: return launch_geom<64, 1>(op, a, waves_per_wg, s);
+        case 2: return launch_geom<64, 2>(op, a, waves_per_wg, s);
+        case 3:
+        case 4: return launch_geom<64, 4>(op, a, waves_per_wg, s);
+        default: return launch_geom<64, 8>(op, a, waves_per_wg, s);
+    }
+}
+
+hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
+                          int64_t chain_offset, mh_summary* out, hipStream_t s) {
+    hipLaunchKernelGGL(mh_summary_kernel, dim3(1), dim3(1024), 0, s, costs, meta, n, chain_offset, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
+                      float* nrm, hipStream_t s) {
+    hipLaunchKernelGGL(mh_rng_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+    return hipGetLastError();
+}
+
+}  // namespace mh

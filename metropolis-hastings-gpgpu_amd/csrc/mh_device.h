@@ -1,0 +1,121 @@
+// mh_device.h -- POD layouts shared by the host library (mh_abi.cpp) and the HIP kernels
+// (mh_chain.hip). Everything here is derived on the host from the KernelWrapper inputs
+// (Kernel.cu:873) so the device never re-derives per-room constants.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define MH_HD __host__ __device__
+#else
+#define MH_HD
+#endif
+
+namespace mh {
+
+// Reference constants, Kernel.cu:31-39 (PI is 3.1416, not M_PI).
+constexpr double kPI = 3.1416;
+constexpr double kTwoPI = 2 * 3.1416;
+constexpr double kHalfPI = 3.1416 / 2.0;
+constexpr double kSigmaT = 15.0 / 90.0 * 3.1416;
+constexpr double kBeta = 2.0;
+
+// Axis-aligned box of a four-vertex rectangle as minValue/maxValue (Kernel.cu:366-401) see it,
+// reduced on the host: for a translation (tx, ty) the box is
+//   min.x = min(v0x, rn_d(xmin1 + tx))   (the first vertex enters untranslated, Kernel.cu:371)
+//   max.x = rn_d(xmax + tx), min.y = rn_d(ymin + ty), max.y = rn_d(ymax + ty)
+// and is then rounded to float (calculateIntersectionArea's fmaxf/fminf, Kernel.cu:325-328).
+// Rounding is monotone, so the running min/max of the reference equals these closed forms.
+struct RectShape {
+    float v0x;  // (float) of vertex 0's x
+    int pad;
+    double xmin1;  // min over vertices 1..3 of x
+    double xmax;   // max over vertices 0..3 of x
+    double ymin;   // min over vertices 0..3 of y
+    double ymax;
+};
+
+struct ObjConst {   // one per object
+    RectShape off;  // its off-limits rectangle (offlimits[j].point1Index)
+    float area;     // (float)(length * width), VisualBalanceCosts Kernel.cu:199
+    int frozen;
+};
+
+struct ClrConst {   // one per clearance
+    RectShape shape;
+    int src;        // clearances[i].SourceIndex
+    int pad;
+};
+
+struct RelConst {   // relationship i: rss[i] and rsa[i] (sized by nRelationships, Kernel.cu:880,885)
+    double start, end;  // rss[i].TargetRange
+    double amin, amax;  // rsa[i].angleMin / angleMax
+    int s, t;           // rss[i] Source / Target
+    int as, at;         // rsa[i] Source / Target
+};
+
+// Scalars of one room, passed by value as a kernel argument.
+struct DevRoom {
+    int n, c, r, pad0;
+    float w_pw, w_vb, w_fp, w_sym, w_ol, w_cl, w_sa;
+    float fxf, fyf;    // (float)focalX, (float)focalY: phi() arguments, Kernel.cu:271
+    float ux, uy;      // (float)cos(focalRot), (float)sin(focalRot), Kernel.cu:290-291
+    float cxf, cyf;    // (float)(centroidX / 2), (float)(centroidY / 2), Kernel.cu:206
+    float denom;       // sequential float sum of areas, Kernel.cu:202
+    float sx, sy;      // proposal std devs width/16, height/16, Kernel.cu:587-591
+    float pad1;
+    double along_f;        // focalX*ux + focalY*uy, Kernel.cu:292
+    double two_focal_rot;  // 2 * focalRot, Kernel.cu:297
+    double rmin_x, rmin_y, rmax_x, rmax_y;  // room box for the translate clamp, Kernel.cu:613-630
+    float comp[4][4];      // complement rectangles (minx, miny, maxx, maxy) as floats, Kernel.cu:343-364
+};
+
+// Per-chain persistent state besides the poses.
+struct ChainMeta {
+    uint64_t draws;     // Philox outputs consumed so far (rocrand offset)
+    uint64_t accepted;  // accepted proposals so far
+    int bm_has;         // Box-Muller cache flag
+    float bm_val;       // cached second normal
+    float costs[8];     // resultCosts of the current state
+    int pad[2];
+};
+static_assert(sizeof(ChainMeta) == 64, "ChainMeta");
+
+// Pose layout in HBM: chain-major, six SoA rows of N doubles.
+enum { F_X = 0, F_Y = 1, F_Z = 2, F_RX = 3, F_RY = 4, F_RZ = 5, F_COUNT = 6 };
+
+// LDS carve-up. One workgroup = WAVES waves; each wave holds G = 64/L chains.
+struct ChainLds {
+    int hdr;     // bytes of the per-workgroup header (frozen flags)
+    int P;       // ObjP[N]   {float xf, yf; double rotY}
+    int X, Y;    // double[N]
+    int Z, RX, RZ;
+    int OFF;     // float4[N] off-limits boxes of the current configuration
+    int CLA;     // float4[C] clearance boxes at their source objects
+    int AUX;     // ChainAux: proposal backups and the current costs
+    int stride;  // bytes per chain
+};
+
+inline MH_HD int round16(int v) { return (v + 15) & ~15; }
+
+inline MH_HD ChainLds make_lds_layout(int n, int c, int L) {
+    ChainLds l;
+    l.hdr = round16(n + 1);
+    int o = 0;
+    l.P = o;   o += round16(16 * n);
+    l.X = o;   o += round16(8 * n);
+    l.Y = o;   o += round16(8 * n);
+    l.Z = o;   o += round16(8 * n);
+    l.RX = o;  o += round16(8 * n);
+    l.RZ = o;  o += round16(8 * n);
+    l.OFF = o; o += round16(16 * n);
+    l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
+    l.AUX = o; o += 192;
+    (void)L;
+    o = round16(o);
+    if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
+    l.stride = o;
+    return l;
+}
+
+}  // namespace mh

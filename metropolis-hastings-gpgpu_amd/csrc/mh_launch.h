@@ -1,0 +1,43 @@
+// mh_launch.h -- launch interface between the host library (mh_abi.cpp) and the HIP kernels
+// (mh_chain.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mh_device.h"
+#include "../../include/mh_kernel.h"
+
+namespace mh {
+
+enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3 };
+
+struct LaunchArgs {
+    DevRoom rm;
+    const ObjConst* objc;
+    const ClrConst* clrc;
+    const RelConst* relc;
+    const double* cfg;       // OP_INIT: [6][N] initial pose; OP_EVAL: [n_chains][6][N]
+    double* st;              // [n_chains][6][N] chain poses
+    ChainMeta* meta;         // [n_chains]
+    point* pts;              // OP_FINAL: [n_chains][N]
+    resultCosts* costs;      // OP_FINAL / OP_EVAL: [n_chains]
+    int64_t n_chains;
+    int64_t chain_offset;    // global id of local chain 0 (Philox subsequence)
+    uint64_t seed;
+    int iterations;
+    ChainLds lay;
+};
+
+int choose_lanes(int n);
+int choose_npl(int n, int L);
+int max_npl();
+size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg);
+hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
+hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
+                          int64_t chain_offset, mh_summary* out, hipStream_t s);
+hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
+                      float* nrm, hipStream_t s);
+
+}  // namespace mh

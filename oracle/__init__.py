@@ -1,0 +1,150 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes loader for the C restatement in mh_oracle.c.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module. The
+product (libmhgpu.so) never loads it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "_build" / "liboracle.so"
+SOURCES = [ORACLE_DIR / "mh_oracle.c"]
+CFLAGS = ["-O2", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+          "-pthread"]
+
+_lib = None
+
+
+def build(force: bool = False) -> Path:
+    import subprocess
+    LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in SOURCES + [ORACLE_DIR / "mh_oracle.h"])
+    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
+        cmd = ["gcc", *CFLAGS, *map(str, SOURCES), "-o", str(LIB_PATH), "-lm"]
+        subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def load(pkg=None) -> C.CDLL:
+    """Loads liboracle.so (building it with gcc if needed). `pkg` is the product package whose
+    ctypes struct mirrors are reused for the argument types."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        build()
+    lib = C.CDLL(str(LIB_PATH))
+    P = C.POINTER
+    lib.orc_costs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.orc_costs.restype = None
+    lib.orc_validate.argtypes = [C.c_void_p, C.c_void_p]
+    lib.orc_validate.restype = C.c_int
+    lib.orc_last_error.restype = C.c_char_p
+    for name, rt in [("orc_visual_balance", C.c_double), ("orc_pairwise", C.c_double),
+                     ("orc_pairwise_angle", C.c_double), ("orc_focal_point", C.c_double),
+                     ("orc_symmetry", C.c_float), ("orc_clearance", C.c_float),
+                     ("orc_surface_area", C.c_float), ("orc_off_limits", C.c_float)]:
+        f = getattr(lib, name)
+        f.argtypes = [C.c_void_p, C.c_void_p]
+        f.restype = rt
+    lib.orc_philox_stream.argtypes = [C.c_uint64, C.c_uint64, P(C.c_uint32), C.c_int]
+    lib.orc_philox_stream.restype = None
+    lib.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+    lib.orc_philox4x32_10.restype = None
+    lib.orc_rng_init.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+    lib.orc_rng_next.argtypes = [C.c_void_p]
+    lib.orc_rng_next.restype = C.c_uint32
+    lib.orc_rng_uniform.argtypes = [C.c_void_p]
+    lib.orc_rng_uniform.restype = C.c_float
+    lib.orc_rng_normal.argtypes = [C.c_void_p]
+    lib.orc_rng_normal.restype = C.c_float
+    lib.orc_run_chains.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int64, C.c_int64,
+                                   C.c_int, C.c_int, C.c_void_p, C.c_void_p, P(C.c_int64)]
+    lib.orc_run_chains.restype = C.c_int
+    lib.orc_run_chains_state.argtypes = lib.orc_run_chains.argtypes
+    lib.orc_run_chains_state.restype = C.c_int
+    lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.orc_accept.argtypes = [C.c_double, C.c_double, C.c_void_p]
+    lib.orc_accept.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+class OrcRoom(C.Structure):
+    _fields_ = [("rs", C.c_void_p), ("ra", C.c_void_p), ("clearances", C.c_void_p),
+                ("offlimits", C.c_void_p), ("vertices", C.c_void_p),
+                ("surfaceRectangle", C.c_void_p), ("srf", C.c_void_p)]
+
+
+class OrcRng(C.Structure):
+    _fields_ = [("counter", C.c_uint32 * 4), ("result", C.c_uint32 * 4), ("key", C.c_uint32 * 2),
+                ("substate", C.c_uint32), ("bm_has", C.c_int32), ("bm_val", C.c_float)]
+
+
+def orc_room(room) -> OrcRoom:
+    """Wraps a product Room (ctypes arrays) for the oracle; keeps `room` alive via ._keep."""
+    r = OrcRoom(C.cast(room.rss, C.c_void_p), C.cast(room.rsa, C.c_void_p),
+                C.cast(room.clearances, C.c_void_p), C.cast(room.offlimits, C.c_void_p),
+                C.cast(room.vertices, C.c_void_p), C.cast(room.surface_rectangle, C.c_void_p),
+                C.cast(C.pointer(room.srf), C.c_void_p))
+    r._keep = room
+    return r
+
+
+def costs(room, cfg=None) -> np.ndarray:
+    """orc_costs -> float32[8] in resultCosts order."""
+    lib = load()
+    out = (C.c_float * 8)()
+    lib.orc_costs(C.byref(orc_room(room)), C.cast(room.cfg if cfg is None else cfg, C.c_void_p),
+                  out)
+    return np.frombuffer(bytes(out), dtype=np.float32).copy()
+
+
+def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int = 0,
+               threads: int = 1, state: bool = False):
+    """Runs the restated chain loop. Returns (points [chains,N,6] float32 or state
+    [chains,N,9] float64 (x,y,z,rotX,rotY,rotZ,frozen,length,width), costs [chains,8] float32,
+    accepted [chains] int64)."""
+    lib = load()
+    n = room.n
+    cs = (C.c_float * (8 * chains))()
+    acc = (C.c_int64 * chains)()
+    if state:
+        from numpy.lib import recfunctions  # noqa: F401
+        buf = (C.c_uint8 * (72 * n * chains))()
+        rc = lib.orc_run_chains_state(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p), seed,
+                                      chain_begin, chains, iterations, threads,
+                                      C.cast(buf, C.c_void_p), C.cast(cs, C.c_void_p), acc)
+    else:
+        buf = (C.c_float * (6 * n * chains))()
+        rc = lib.orc_run_chains(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p), seed,
+                                chain_begin, chains, iterations, threads,
+                                C.cast(buf, C.c_void_p), C.cast(cs, C.c_void_p), acc)
+    if rc != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    c8 = np.frombuffer(bytes(cs), dtype=np.float32).reshape(chains, 8).copy()
+    a = np.frombuffer(bytes(acc), dtype=np.int64).copy()
+    if state:
+        raw = np.frombuffer(bytes(buf), dtype=np.uint8).reshape(chains, n, 72)
+        d = np.zeros((chains, n, 6), dtype=np.float64)
+        for k in range(6):
+            d[:, :, k] = raw[:, :, 8 * k:8 * k + 8].copy().view(np.float64)[:, :, 0]
+        return d, c8, a
+    return np.frombuffer(bytes(buf), dtype=np.float32).reshape(chains, n, 6).copy(), c8, a
+
+
+def rng_streams(seed: int, subsequence: int, n: int):
+    """(u32, uniform, normal) streams, each restarted at draw 0 (as mh_debug_rng)."""
+    lib = load()
+    u = (C.c_uint32 * n)()
+    lib.orc_philox_stream(seed, subsequence, u, n)
+    r = OrcRng()
+    lib.orc_rng_init(C.byref(r), seed, subsequence)
+    f = np.array([lib.orc_rng_uniform(C.byref(r)) for _ in range(n)], dtype=np.float32)
+    lib.orc_rng_init(C.byref(r), seed, subsequence)
+    g = np.array([lib.orc_rng_normal(C.byref(r)) for _ in range(n)], dtype=np.float32)
+    return np.frombuffer(bytes(u), dtype=np.uint32).copy(), f, g

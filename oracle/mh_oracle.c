@@ -1,0 +1,609 @@
+/*
+ * mh_oracle.c -- TEST INFRASTRUCTURE ONLY (see mh_oracle.h).
+ *
+ * A plain-C restatement of the reference's per-chain hot path, Kernel.cu:162-828, written to
+ * reproduce its arithmetic exactly: every value the reference holds in a float is rounded to a
+ * float here at the same point, every double stays a double, and sums are taken in the
+ * reference's loop order. Build with -ffp-contract=off (no fused multiply-add anywhere).
+ *
+ * Math library contract (shared with the device; DESIGN.md "Numerics"):
+ *   - sqrt/sqrtf/division: IEEE correctly rounded on both sides;
+ *   - the reference's float transcendentals (atan2f in phi, cosf in FocalPointCosts) are taken
+ *     as the double function rounded once to float, which is what a correctly rounded float
+ *     library returns except in ~2^-29 of cases;
+ *   - double transcendentals (atan2 in theta, cos/sin of focalRot, exp in Accept, log/sin/cos in
+ *     Box-Muller) come from libm here and from OCML on the device; both are within ~1 ulp.
+ *
+ * Defined semantics where the reference is ill-defined:
+ *   - one proposer per chain and a full state copy each step (the reference races when
+ *     blockDim.x > 1, Kernel.cu:798, and copies with a broken stride, :733-734);
+ *   - a drawn index == nObjs (u == 1.0f with nObjs >= 64, :566-574) counts as frozen and is
+ *     redrawn; all-frozen rooms are a validation error instead of an endless loop (:600-602);
+ *   - the chain's result is its final current state plus that state's cost components.
+ */
+#define _GNU_SOURCE
+#include "mh_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* Constants, Kernel.cu:31-39. PI is 3.1416, not M_PI. */
+#define ORC_PI (3.1416)
+#define ORC_BETA (2.0)
+#define ORC_S_SIGMA_T (15.0 / 90.0 * ORC_PI)
+
+static __thread char g_err[256];
+
+const char* orc_last_error(void) { return g_err; }
+
+static int fail(const char* msg, long a) {
+    snprintf(g_err, sizeof g_err, msg, a);
+    return -1;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * RNG: rocRAND philox4x32_10_engine (rocrand_philox4x32_10.h), restated.
+ * key = seed (lo, hi); counter = (0, 0, subsequence lo, subsequence hi); each block of four
+ * outputs is ten Random123 Philox rounds of the counter; the counter then increments.
+ * ---------------------------------------------------------------------------------------- */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int round = 0; round < 10; ++round) {
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += PHILOX_W0;
+        k1 += PHILOX_W1;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void rng_refill(orc_rng* r) { orc_philox4x32_10(r->counter, r->key, r->result); }
+
+static void rng_bump(orc_rng* r) {
+    if (++r->counter[0] != 0) return;
+    if (++r->counter[1] != 0) return;
+    if (++r->counter[2] != 0) return;
+    ++r->counter[3];
+}
+
+void orc_rng_init(orc_rng* r, uint64_t seed, uint64_t subsequence) {
+    memset(r, 0, sizeof *r);
+    r->key[0] = (uint32_t)seed;
+    r->key[1] = (uint32_t)(seed >> 32);
+    r->counter[2] = (uint32_t)subsequence;
+    r->counter[3] = (uint32_t)(subsequence >> 32);
+    rng_refill(r);
+}
+
+uint32_t orc_rng_next(orc_rng* r) {
+    uint32_t v = r->result[r->substate];
+    if (++r->substate == 4) {
+        r->substate = 0;
+        rng_bump(r);
+        rng_refill(r);
+    }
+    return v;
+}
+
+/* rocrand_uniform (rocrand_uniform.h uniform_distribution): (0, 1], float arithmetic. Plays
+ * the role of curand_uniform at Kernel.cu:569,710. */
+float orc_rng_uniform(orc_rng* r) {
+    const float inv = 2.3283064e-10f;
+    float v = (float)orc_rng_next(r);
+    float scaled = v * inv;
+    return inv + scaled;
+}
+
+/* Normal draw standing in for curand_normal (Kernel.cu:605,608,641): Box-Muller on two
+ * uniforms in (0,1) evaluated in double and rounded to float; the sine branch is returned
+ * first and the cosine branch is cached for the next call, as cuRAND's Box-Muller does. */
+float orc_rng_normal(orc_rng* r) {
+    if (r->bm_has) {
+        r->bm_has = 0;
+        return r->bm_val;
+    }
+    uint32_t a = orc_rng_next(r);
+    uint32_t b = orc_rng_next(r);
+    double u1 = (double)a * 0x1p-32 + 0x1p-33;
+    double u2 = (double)b * 0x1p-32 + 0x1p-33;
+    double rad = sqrt(-2.0 * log(u1));
+    double ang = 6.283185307179586 * u2;
+    r->bm_val = (float)(rad * cos(ang));
+    r->bm_has = 1;
+    return (float)(rad * sin(ang));
+}
+
+void orc_philox_stream(uint64_t seed, uint64_t subsequence, uint32_t* out, int n) {
+    orc_rng r;
+    orc_rng_init(&r, seed, subsequence);
+    for (int i = 0; i < n; ++i) out[i] = orc_rng_next(&r);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Geometry helpers.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct { double x, y; } dvec2;
+
+/* Kernel.cu:162-167: the difference is taken in float, the root in double. */
+static double distance_f(float xi, float yi, float xj, float yj) {
+    float fx = xi - xj;
+    float fy = yi - yj;
+    double dx = fx, dy = fy;
+    double sq = dx * dx;
+    sq = sq + dy * dy;
+    return sqrt(sq);
+}
+
+/* Kernel.cu:170-182: bearing of i->j relative to ti, wrapped to [0, 2*PI) with PI = 3.1416. */
+static double theta_f(float xi, float yi, float xj, float yj, float ti) {
+    double dx = (double)(float)(xi - xj);
+    double dy = (double)(float)(yi - yj);
+    double tp = atan2(dy, dx);
+    if (tp < 0) tp = 2 * ORC_PI + tp;
+    double t = tp - (double)ti;
+    return (t < 0) ? 2 * ORC_PI + t : t;
+}
+
+/* float atan2 / cos as the double function rounded once (see header comment). */
+static float atan2_f32(float y, float x) { return (float)atan2((double)y, (double)x); }
+static float cos_f32(float x) { return (float)cos((double)x); }
+
+/* Kernel.cu:185-188: atan2 of float differences (float result), minus tj in float, plus
+ * PI/2 in double, rounded to float on return. */
+static float phi_f(float xi, float yi, float xj, float yj, float tj) {
+    float a = atan2_f32(yi - yj, xi - xj);
+    float b = a - tj;
+    return (float)((double)b + ORC_PI / 2.0);
+}
+
+/* Kernel.cu:366-382 minValue: AABB minimum of the four consecutive vertices starting at
+ * `start`, translated by (tx, ty). The first x candidate keeps the UNtranslated vertex
+ * (Kernel.cu:371); y is translated throughout. */
+static dvec2 aabb_min(const vertex* v, int start, float tx, float ty) {
+    dvec2 m = {DBL_MAX, DBL_MAX};
+    const vertex* q = v + start;
+    m.x = (m.x > q[0].x + tx) ? q[0].x : m.x;
+    for (int k = 1; k < 4; ++k) m.x = (m.x > q[k].x + tx) ? q[k].x + tx : m.x;
+    for (int k = 0; k < 4; ++k) m.y = (m.y > q[k].y + ty) ? q[k].y + ty : m.y;
+    return m;
+}
+
+/* Kernel.cu:384-401 maxValue: the translated maximum. */
+static dvec2 aabb_max(const vertex* v, int start, float tx, float ty) {
+    dvec2 m = {-DBL_MAX, -DBL_MAX};
+    const vertex* q = v + start;
+    for (int k = 0; k < 4; ++k) m.x = (m.x < q[k].x + tx) ? q[k].x + tx : m.x;
+    for (int k = 0; k < 4; ++k) m.y = (m.y < q[k].y + ty) ? q[k].y + ty : m.y;
+    return m;
+}
+
+/* Kernel.cu:321-340: overlap area of two AABBs; the double corners pass through fmaxf/fminf,
+ * i.e. are rounded to float (so +-DBL_MAX becomes +-inf). */
+static float overlap_area(dvec2 amin, dvec2 amax, dvec2 bmin, dvec2 bmax) {
+    float x5 = fmaxf((float)amin.x, (float)bmin.x);
+    float y5 = fmaxf((float)amin.y, (float)bmin.y);
+    float x6 = fminf((float)amax.x, (float)bmax.x);
+    float y6 = fminf((float)amax.y, (float)bmax.y);
+    if (x5 >= x6 || y5 >= y6) return 0.0f;
+    return (x6 - x5) * (y6 - y5);
+}
+
+/* Kernel.cu:343-364: the complement of the room AABB as four rectangles (min, max). */
+static void complement_rects(dvec2 rmin, dvec2 rmax, dvec2 cmin[4], dvec2 cmax[4]) {
+    cmin[0] = (dvec2){-DBL_MAX, -DBL_MAX}; cmax[0] = (dvec2){DBL_MAX, rmin.y};
+    cmin[1] = (dvec2){-DBL_MAX, rmin.y};   cmax[1] = (dvec2){rmin.x, rmax.y};
+    cmin[2] = (dvec2){-DBL_MAX, rmax.y};   cmax[2] = (dvec2){DBL_MAX, DBL_MAX};
+    cmin[3] = (dvec2){rmax.x, rmin.y};     cmax[3] = (dvec2){DBL_MAX, rmax.y};
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Cost terms, Kernel.cu:191-514.
+ * ---------------------------------------------------------------------------------------- */
+
+/* Kernel.cu:191-207. Accumulators are floats updated through double temporaries. */
+double orc_visual_balance(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    float nx = 0, ny = 0, denom = 0;
+    for (int i = 0; i < s->nObjs; ++i) {
+        float area = (float)(cfg[i].length * cfg[i].width);
+        nx = (float)((double)nx + (double)area * cfg[i].x);
+        ny = (float)((double)ny + (double)area * cfg[i].y);
+        denom = denom + area;
+    }
+    return -1.0 * distance_f(nx / denom, ny / denom, (float)(s->centroidX / 2),
+                             (float)(s->centroidY / 2));
+}
+
+/* Kernel.cu:210-233. */
+double orc_pairwise(const orc_room* room, const positionAndRotation* cfg) {
+    double acc = 0;
+    for (int i = 0; i < room->srf->nRelationships; ++i) {
+        const relationshipStruct* r = &room->rs[i];
+        const positionAndRotation* a = &cfg[r->SourceIndex];
+        const positionAndRotation* b = &cfg[r->TargetIndex];
+        double d = distance_f((float)a->x, (float)a->y, (float)b->x, (float)b->y);
+        if (d < r->TargetRange.targetRangeStart) {
+            double f = d / r->TargetRange.targetRangeStart;
+            acc -= f * f;
+        } else if (d > r->TargetRange.targetRangeEnd) {
+            double f = r->TargetRange.targetRangeEnd / d;
+            acc -= f * f;
+        }
+    }
+    return acc;
+}
+
+/* Kernel.cu:236-263, including the wrap branch's fmodf and the `min < d || d < max`
+ * condition of the plain branch exactly as written. */
+double orc_pairwise_angle(const orc_room* room, const positionAndRotation* cfg) {
+    double acc = 0;
+    for (int i = 0; i < room->srf->nRelationships; ++i) {
+        const relationshipAngleStruct* r = &room->ra[i];
+        const positionAndRotation* a = &cfg[r->SourceIndex];
+        const positionAndRotation* b = &cfg[r->TargetIndex];
+        double d = theta_f((float)a->x, (float)a->y, (float)b->x, (float)b->y, (float)b->rotY);
+        double lo = r->angleMin, hi = r->angleMax;
+        if (lo > hi) {
+            double norm = (2 * ORC_PI - (hi + (2 * ORC_PI - lo))) / 2.0;
+            float wrapped = fmodf((float)(lo + d), (float)(2 * ORC_PI));
+            if ((double)wrapped > hi) acc -= fmin(fabs(d - lo), fabs(d - hi)) / norm;
+        } else if (lo < d || d < hi) {
+            double norm = (2 * ORC_PI - (hi - lo)) / 2.0;
+            acc -= fmin(fabs(d - lo), fabs(d - hi)) / norm;
+        }
+    }
+    return acc;
+}
+
+/* Kernel.cu:266-281. */
+double orc_focal_point(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    double acc = 0;
+    for (int i = 0; i < s->nObjs; ++i) {
+        float p = phi_f((float)s->focalX, (float)s->focalY, (float)cfg[i].x, (float)cfg[i].y,
+                        (float)cfg[i].rotY);
+        acc -= (double)cos_f32(p);
+    }
+    return acc;
+}
+
+/* Kernel.cu:283-318. Reflect object i across the focal axis; score the best-matching j. */
+float orc_symmetry(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    const int n = s->nObjs;
+    float acc = 0;
+    for (int i = 0; i < n; ++i) {
+        float best = 0;
+        float ux = (float)cos(s->focalRot);
+        float uy = (float)sin(s->focalRot);
+        double along_f = s->focalX * ux;
+        along_f = along_f + s->focalY * uy;
+        double along_i = cfg[i].x * ux;
+        along_i = along_i + cfg[i].y * uy;
+        float sd = (float)(2 * (along_f - along_i));
+        float rx = (float)(cfg[i].x + (double)(sd * ux));
+        float ry = (float)(cfg[i].y + (double)(sd * uy));
+        float rrot = (float)(2 * s->focalRot - cfg[i].rotY);
+        if (rrot < -ORC_PI) rrot = (float)((double)rrot + 2 * ORC_PI);
+        for (int j = 0; j < n; ++j) {
+            float dp = (float)distance_f((float)cfg[j].x, (float)cfg[j].y, rx, ry);
+            float dt = (float)(cfg[j].rotY - (double)rrot);
+            if (dt > ORC_PI) dt = (float)((double)dt - 2 * ORC_PI);
+            float head = 5.0f - sqrtf(dp);
+            float val = (float)((double)head - 0.4 * (double)fabsf(dt));
+            best = fmaxf(best, val);
+        }
+        acc = acc - best;
+    }
+    return acc;
+}
+
+/* Kernel.cu:404-434: every clearance (at its source object) against every object's
+ * off-limits rectangle, the source object included; float sum in i-major order. */
+float orc_clearance(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    float err = 0.0f;
+    for (int i = 0; i < s->nClearances; ++i) {
+        const rectangle* c = &room->clearances[i];
+        const positionAndRotation* src = &cfg[c->SourceIndex];
+        for (int j = 0; j < s->nObjs; ++j) {
+            dvec2 amin = aabb_min(room->vertices, c->point1Index, (float)src->x, (float)src->y);
+            dvec2 amax = aabb_max(room->vertices, c->point1Index, (float)src->x, (float)src->y);
+            int o = room->offlimits[j].point1Index;
+            dvec2 bmin = aabb_min(room->vertices, o, (float)cfg[j].x, (float)cfg[j].y);
+            dvec2 bmax = aabb_max(room->vertices, o, (float)cfg[j].x, (float)cfg[j].y);
+            err -= overlap_area(amin, amax, bmin, bmax);
+        }
+    }
+    return err;
+}
+
+/* Kernel.cu:437-483. Clearance i is translated by cfg[i] (not its source, :456). */
+float orc_surface_area(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    dvec2 rmin = aabb_min(room->surfaceRectangle, 0, 0, 0);
+    dvec2 rmax = aabb_max(room->surfaceRectangle, 0, 0, 0);
+    dvec2 cmin[4], cmax[4];
+    complement_rects(rmin, rmax, cmin, cmax);
+    float err = 0.0f;
+    for (int i = 0; i < s->nClearances; ++i) {
+        int p = room->clearances[i].point1Index;
+        dvec2 amin = aabb_min(room->vertices, p, (float)cfg[i].x, (float)cfg[i].y);
+        dvec2 amax = aabb_max(room->vertices, p, (float)cfg[i].x, (float)cfg[i].y);
+        for (int k = 0; k < 4; ++k) err -= overlap_area(amin, amax, cmin[k], cmax[k]);
+    }
+    for (int j = 0; j < s->nObjs; ++j) {
+        int p = room->offlimits[j].point1Index;
+        dvec2 amin = aabb_min(room->vertices, p, (float)cfg[j].x, (float)cfg[j].y);
+        dvec2 amax = aabb_max(room->vertices, p, (float)cfg[j].x, (float)cfg[j].y);
+        for (int k = 0; k < 4; ++k) err -= overlap_area(amin, amax, cmin[k], cmax[k]);
+    }
+    return err;
+}
+
+/* Kernel.cu:485-514: off-limits overlap over unordered pairs i < j. */
+float orc_off_limits(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    float err = 0.0f;
+    for (int i = 0; i < s->nObjs; ++i) {
+        for (int j = i + 1; j < s->nObjs; ++j) {
+            int pi = room->offlimits[i].point1Index, pj = room->offlimits[j].point1Index;
+            dvec2 amin = aabb_min(room->vertices, pi, (float)cfg[i].x, (float)cfg[i].y);
+            dvec2 amax = aabb_max(room->vertices, pi, (float)cfg[i].x, (float)cfg[i].y);
+            dvec2 bmin = aabb_min(room->vertices, pj, (float)cfg[j].x, (float)cfg[j].y);
+            dvec2 bmax = aabb_max(room->vertices, pj, (float)cfg[j].x, (float)cfg[j].y);
+            err -= overlap_area(amin, amax, bmin, bmax);
+        }
+    }
+    return err;
+}
+
+/* Kernel.cu:516-550. PairWise is the PRODUCT of the distance and angle terms (:518); the
+ * total leaves OffLimits out (:547) and is summed in float in the reference's order. */
+void orc_costs(const orc_room* room, const positionAndRotation* cfg, resultCosts* out) {
+    const Surface* s = room->srf;
+    float pw = (float)(orc_pairwise(room, cfg) * orc_pairwise_angle(room, cfg));
+    out->PairWiseCosts = s->WeightPairWise * pw;
+    float vb = (float)orc_visual_balance(room, cfg);
+    out->VisualBalanceCosts = s->WeightVisualBalance * vb;
+    float fp = (float)orc_focal_point(room, cfg);
+    out->FocalPointCosts = s->WeightFocalPoint * fp;
+    float sym = orc_symmetry(room, cfg);
+    out->SymmetryCosts = s->WeightSymmetry * sym;
+    float ol = orc_off_limits(room, cfg);
+    out->OffLimitsCosts = s->WeightOffLimits * ol;
+    float cl = orc_clearance(room, cfg);
+    out->ClearanceCosts = s->WeightClearance * cl;
+    float sa = orc_surface_area(room, cfg);
+    out->SurfaceAreaCosts = s->WeightSurfaceArea * sa;
+    float t = out->PairWiseCosts + out->VisualBalanceCosts;
+    t = t + out->FocalPointCosts;
+    t = t + out->SymmetryCosts;
+    t = t + out->ClearanceCosts;
+    t = t + out->SurfaceAreaCosts;
+    out->totalCosts = t;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * MH step, Kernel.cu:566-713.
+ * ---------------------------------------------------------------------------------------- */
+
+/* Kernel.cu:566-574: u in (0,1] scaled by (max - min + 0.999999) in double, kept as a float,
+ * truncated. With max = nObjs - 1 >= 63, u == 1.0f yields nObjs. */
+static int rand_int(orc_rng* r, int max, int min) {
+    float u = orc_rng_uniform(r);
+    u = (float)((double)u * ((double)(max - min) + 0.999999));
+    u = u + (float)min;
+    return (int)truncf(u);
+}
+
+/* Object pick with redraw while frozen (Kernel.cu:598-602); index nObjs is frozen. */
+static int pick_object(const positionAndRotation* cfg, int n, orc_rng* r) {
+    int k = rand_int(r, n - 1, 0);
+    while (k >= n || cfg[k].frozen) k = rand_int(r, n - 1, 0);
+    return k;
+}
+
+void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r) {
+    const int n = room->srf->nObjs;
+    int mode = rand_int(r, 2, 0);
+    dvec2 rmin = aabb_min(room->surfaceRectangle, 0, 0, 0);
+    dvec2 rmax = aabb_max(room->surfaceRectangle, 0, 0, 0);
+    float width = (float)(rmax.x - rmin.x);
+    float height = (float)(rmax.y - rmin.y);
+    float sx = width / 16;
+    float sy = height / 16;
+    if (mode == 0) { /* translate, Kernel.cu:595-632 */
+        int k = pick_object(cfg, n, r);
+        float dx = orc_rng_normal(r);
+        dx = dx * sx;
+        float dy = orc_rng_normal(r);
+        dy = dy * sy;
+        positionAndRotation* o = &cfg[k];
+        if (o->x + dx > rmax.x) o->x = rmax.x;
+        else if (o->x + dx < rmin.x) o->x = rmin.x;
+        else o->x = o->x + dx;
+        if (o->y + dy > rmax.y) o->y = rmax.y;
+        else if (o->y + dy < rmin.y) o->y = rmin.y;
+        else o->y = o->y + dy;
+    } else if (mode == 1) { /* rotate, Kernel.cu:634-653 */
+        int k = pick_object(cfg, n, r);
+        float dr = orc_rng_normal(r);
+        dr = (float)(dr * ORC_S_SIGMA_T);
+        positionAndRotation* o = &cfg[k];
+        o->rotY = o->rotY + dr;
+        if (o->rotY < 0) o->rotY = o->rotY + 2 * ORC_PI;
+        else if (o->rotY > 2 * ORC_PI) o->rotY = o->rotY - 2 * ORC_PI;
+    } else { /* swap, Kernel.cu:655-703; object 1's pose travels through floats */
+        if (n < 2) return;
+        int a = pick_object(cfg, n, r);
+        int b = pick_object(cfg, n, r);
+        positionAndRotation* p = &cfg[a];
+        positionAndRotation* q = &cfg[b];
+        float t[6] = {(float)p->x, (float)p->y, (float)p->z,
+                      (float)p->rotX, (float)p->rotY, (float)p->rotZ};
+        p->x = q->x; p->y = q->y; p->z = q->z;
+        p->rotX = q->rotX; p->rotY = q->rotY; p->rotZ = q->rotZ;
+        q->x = t[0]; q->y = t[1]; q->z = t[2];
+        q->rotX = t[3]; q->rotY = t[4]; q->rotZ = t[5];
+    }
+}
+
+/* Kernel.cu:706-713: maximises the total; exp in double, rounded to float. */
+int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
+    float u = orc_rng_uniform(r);
+    float a = fminf(1.0f, (float)exp(ORC_BETA * (cost_star - cost_cur)));
+    return u < a;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Validation (the reference performs none; see mh_kernel.h).
+ * ---------------------------------------------------------------------------------------- */
+int orc_validate(const orc_room* room, const positionAndRotation* cfg) {
+    const Surface* s = room->srf;
+    if (!s) return fail("srf is NULL%ld", 0);
+    const int n = s->nObjs, c = s->nClearances, nr = s->nRelationships;
+    if (n < 1) return fail("nObjs must be >= 1 (got %ld)", n);
+    if (c < 0 || c > n) return fail("nClearances must be in [0, nObjs] (got %ld)", c);
+    if (nr < 0) return fail("nRelationships must be >= 0 (got %ld)", nr);
+    if (!cfg || !room->offlimits || !room->vertices || !room->surfaceRectangle)
+        return fail("NULL input array%ld", 0);
+    if ((nr > 0 && (!room->rs || !room->ra)) || (c > 0 && !room->clearances))
+        return fail("NULL input array%ld", 0);
+    const long nv = 4L * (c + n);
+    int any_free = 0;
+    for (int i = 0; i < n; ++i) {
+        int p = room->offlimits[i].point1Index;
+        if (p < 0 || p + 3 >= nv) return fail("offlimits[%ld].point1Index out of range", i);
+        if (!cfg[i].frozen) any_free = 1;
+    }
+    if (!any_free) return fail("every object is frozen (the reference never terminates)%ld", 0);
+    for (int i = 0; i < c; ++i) {
+        int p = room->clearances[i].point1Index, q = room->clearances[i].SourceIndex;
+        if (p < 0 || p + 3 >= nv) return fail("clearances[%ld].point1Index out of range", i);
+        if (q < 0 || q >= n) return fail("clearances[%ld].SourceIndex out of range", i);
+    }
+    for (int i = 0; i < nr; ++i) {
+        if (room->rs[i].SourceIndex < 0 || room->rs[i].SourceIndex >= n ||
+            room->rs[i].TargetIndex < 0 || room->rs[i].TargetIndex >= n)
+            return fail("rss[%ld] index out of range", i);
+        if (room->ra[i].SourceIndex < 0 || room->ra[i].SourceIndex >= n ||
+            room->ra[i].TargetIndex < 0 || room->ra[i].TargetIndex >= n)
+            return fail("rsa[%ld] index out of range", i);
+    }
+    g_err[0] = 0;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Chains, Kernel.cu:777-828 with the defined semantics of the header.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    const orc_room* room;
+    const positionAndRotation* cfg;
+    uint64_t seed;
+    int64_t chain_begin;
+    int64_t lo, hi; /* local chain range for this worker */
+    int iterations;
+    point* out_points;
+    positionAndRotation* out_state;
+    resultCosts* out_costs;
+    int64_t* out_accepted;
+} chain_job;
+
+static void run_one(const chain_job* job, int64_t local, positionAndRotation* cur,
+                    positionAndRotation* star) {
+    const int n = job->room->srf->nObjs;
+    orc_rng r;
+    orc_rng_init(&r, job->seed, (uint64_t)(job->chain_begin + local));
+    memcpy(cur, job->cfg, sizeof(positionAndRotation) * n);
+    resultCosts cc, sc;
+    orc_costs(job->room, cur, &cc);
+    int64_t acc = 0;
+    for (int it = 0; it < job->iterations; ++it) {
+        memcpy(star, cur, sizeof(positionAndRotation) * n);
+        orc_propose(job->room, star, &r);
+        orc_costs(job->room, star, &sc);
+        if (orc_accept(sc.totalCosts, cc.totalCosts, &r)) {
+            memcpy(cur, star, sizeof(positionAndRotation) * n);
+            cc = sc;
+            ++acc;
+        }
+    }
+    if (job->out_points) {
+        point* p = job->out_points + local * n;
+        for (int i = 0; i < n; ++i) {
+            p[i].x = (float)cur[i].x; p[i].y = (float)cur[i].y; p[i].z = (float)cur[i].z;
+            p[i].rotX = (float)cur[i].rotX; p[i].rotY = (float)cur[i].rotY;
+            p[i].rotZ = (float)cur[i].rotZ;
+        }
+    }
+    if (job->out_state) memcpy(job->out_state + local * n, cur, sizeof(positionAndRotation) * n);
+    if (job->out_costs) job->out_costs[local] = cc;
+    if (job->out_accepted) job->out_accepted[local] = acc;
+}
+
+static void* chain_worker(void* arg) {
+    const chain_job* job = (const chain_job*)arg;
+    const int n = job->room->srf->nObjs;
+    positionAndRotation* cur = malloc(sizeof(positionAndRotation) * n);
+    positionAndRotation* star = malloc(sizeof(positionAndRotation) * n);
+    for (int64_t c = job->lo; c < job->hi; ++c) run_one(job, c, cur, star);
+    free(cur);
+    free(star);
+    return NULL;
+}
+
+static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
+                      int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
+                      point* out_points, positionAndRotation* out_state,
+                      resultCosts* out_costs, int64_t* out_accepted) {
+    if (orc_validate(room, cfg) != 0) return -1;
+    if (n_chains < 0 || iterations < 0) return fail("negative chain or step count%ld", 0);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > n_chains) nthreads = (int)(n_chains > 0 ? n_chains : 1);
+    chain_job* jobs = calloc((size_t)nthreads, sizeof(chain_job));
+    pthread_t* th = calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; ++t) {
+        chain_job j = {room, cfg, seed, chain_begin,
+                       n_chains * t / nthreads, n_chains * (t + 1) / nthreads,
+                       iterations, out_points, out_state, out_costs, out_accepted};
+        jobs[t] = j;
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, chain_worker, &jobs[t]);
+    chain_worker(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+int orc_run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
+                   int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
+                   point* out_points, resultCosts* out_costs, int64_t* out_accepted) {
+    return run_chains(room, cfg, seed, chain_begin, n_chains, iterations, nthreads, out_points,
+                      NULL, out_costs, out_accepted);
+}
+
+int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
+                         int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
+                         positionAndRotation* out_state, resultCosts* out_costs,
+                         int64_t* out_accepted) {
+    return run_chains(room, cfg, seed, chain_begin, n_chains, iterations, nthreads, NULL,
+                      out_state, out_costs, out_accepted);
+}
