@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark: MH chain-steps/s on the 64-object synthetic room (BASELINE.json config 3).
+
+One bench "step" = one launch of the chain kernel that advances every chain of this GPU's
+shard by --iters MH steps (propose -> Costs -> accept, Kernel.cu:785-828), state resident in
+HBM/LDS. value = (all ranks' chains) x (timed MH steps) / max-over-ranks wall time.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU, chains sharded by global id (chain c always draws Philox subsequence c), no collective
+on the data path; after sampling one RCCL all-gather of each rank's 40-byte best-cost summary
+selects the global best layout (north_star). Weak scaling: --chains chains per GPU.
+
+Also reported: a VALU roofline for the step kernel (canonical algorithmic
+flops F(N,C,R) per chain-step / measured kernel time vs the 157.3 TFLOP/s FP32 vector peak) and
+the oracle's restatement of the reference chain timed on this host's cores (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import __graft_entry__ as graft  # noqa: E402
+
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (== FP32 MFMA peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_flops(n: int, c: int, r: int) -> int:
+    """canonical flops of one chain-step (full recompute of the accept-relevant
+    cost, off-limits excluded; each sqrt/transcendental counts 1)."""
+    return 14 * n * n + 10 * c * n + 60 * c + 89 * n + 25 * r + 60
+
+
+def state_bytes_per_chain(n: int) -> int:
+    """HBM bytes one launch moves per chain: pose load + store (6 doubles per object) and the
+    64-byte ChainMeta load + store. The room tables are shared and L2-resident."""
+    return 2 * (6 * 8 * n) + 2 * 64
+
+
+def cpu_baseline(room, orc, seed: int, budget_s: float, threads: int):
+    """Oracle chain (the reference's algorithm, Kernel.cu:777-828, OffLimits included as the
+    reference computes it every step) on `threads` host cores, bounded to ~budget_s."""
+    t0 = time.perf_counter()
+    orc.run_chains(room, threads, 20, seed, threads=threads)
+    per = (time.perf_counter() - t0) / (threads * 20) * threads  # seconds per chain-step/thread
+    steps = max(20, int(budget_s / max(per, 1e-9) / 4))
+    chains = 4 * threads
+    t0 = time.perf_counter()
+    orc.run_chains(room, chains, steps, seed, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": chains * steps / dt, "unit": "chain-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/mh_oracle.c chain on {room.name}: {chains} chains x {steps} steps"
+                      f" ({dt:.1f} s, {threads} threads)"}
+
+
+def pmc_traffic(n_chains_per_launch: int):
+    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC pass, if present
+    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py), else None."""
+    p = ROOT / "profiles" / "pmc_step_kernel.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        if int(d.get("chains_per_launch", -1)) != n_chains_per_launch:
+            return None
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed launches")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=1000, help="MH steps per launch (<= 1000)")
+    ap.add_argument("--objects", type=int, default=64)
+    ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    args.iters = max(1, min(args.iters, 1000))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    mh = graft.load_package()
+    mh.load_library()
+    room = mh.synthetic_room(args.objects)
+    n, c, r = room.n, room.srf.nClearances, room.srf.nRelationships
+
+    # A dedicated (non-null) stream: the kernels and the timing events share it.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    handle = stream.cuda_stream
+    assert handle, "need a non-null HIP stream handle"
+    sess = mh.Session(room, args.chains, seed=args.seed, device=local_rank,
+                      chain_offset=rank * args.chains)
+    lanes, cpw = sess.geometry()
+
+    for _ in range(args.warmup):
+        sess.run(args.iters, handle)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        sess.run(args.iters, handle)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1)
+
+    # Final state, summary and the RCCL best-cost all-gather (outside the timed region).
+    sess.finalize(handle)
+    torch.cuda.synchronize()
+    s = sess.summary()
+    rec = torch.tensor([s.sum_total, float(s.best_total), float(s.best_chain),
+                        float(s.n_chains), float(s.accepted)], dtype=torch.float64,
+                       device=f"cuda:{local_rank}")
+    times = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
+    if world > 1:
+        gathered = [torch.empty_like(rec) for _ in range(world)]
+        dist.all_gather(gathered, rec)
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+        recs = torch.stack(gathered).cpu()
+    else:
+        recs = rec.unsqueeze(0).cpu()
+    wall, kernel_ms = float(times[0]), float(times[1])
+    best_rank = int(torch.argmax(recs[:, 1]))
+    total_chains = int(recs[:, 3].sum())
+    mean_cost = float(recs[:, 0].sum()) / total_chains
+    best_cost = float(recs[best_rank, 1])
+    best_chain = int(recs[best_rank, 2])
+    accept_rate = float(recs[:, 4].sum()) / (total_chains * (args.warmup + args.steps) * args.iters)
+
+    chain_steps = total_chains * args.steps * args.iters
+    value = chain_steps / wall
+    ms_per_step = wall * 1e3 / args.steps
+    launch_s = kernel_ms / 1e3 / args.steps  # average duration of one step-kernel launch
+    f = algorithmic_flops(n, c, r)
+    achieved = args.chains * args.iters * f / launch_s / 1e12
+    bytes_launch = args.chains * state_bytes_per_chain(n)
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            orc = graft.load_oracle()
+            threads = max(1, min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(room, orc, args.seed, args.cpu_budget, threads)
+        out = {
+            "metric": "MH chain-steps/sec (whole node) + mean final cost, N=64 objects",
+            "value": value,
+            "unit": "chain-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64+f32 (reference precision map)",
+            "data": "synthetic (SURVEY.md 8(d) room, splitmix64 seed 0x5EED0000+N)",
+            "config": {
+                "workload": f"config 3: {n}-object synthetic room, {args.chains} chains per GPU,"
+                            f" {args.iters} MH steps per launch",
+                "objects": n, "clearances": c, "relationships": r,
+                "chains_per_gpu": args.chains, "global_chains": total_chains,
+                "mh_steps_per_step": args.iters,
+                "mh_steps_total": (args.warmup + args.steps) * args.iters,
+                "lanes_per_chain": lanes, "chains_per_workgroup": cpw,
+                "parallelism": f"chain-sharded x{world} (RCCL best-cost all-gather)",
+            },
+            "mean_final_cost": mean_cost,
+            "best_final_cost": best_cost,
+            "best_chain": best_chain,
+            "accept_rate": accept_rate,
+            "kernel_ms_per_step": kernel_ms / args.steps,
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": FP32_VECTOR_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP32_VECTOR_PEAK_TFLOPS,
+                "traffic": pmc_traffic(args.chains),
+                "flops_per_chain_step": f,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "hbm_frac": bytes_launch / launch_s / 1e9 / HBM_PEAK_GBS,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

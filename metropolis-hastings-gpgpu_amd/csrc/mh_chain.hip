@@ -27,9 +27,10 @@
 
 namespace mh {
 
-struct ObjP {  // per-object pose words read by the O(N^2) symmetry loop: one ds_read_b128
+struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
     float xf, yf;  // (float)x, (float)y -- every O(N^2) use of x, y is through float args
-    double rotY;
+    float rotYf;   // (float)rotY
+    float pad;
 };
 
 struct Backup {
@@ -47,6 +48,8 @@ static_assert(sizeof(ChainAux) <= 192, "ChainAux");
 
 struct ChainPtrs {
     ObjP* P;
+    double* RY;
+    double* SCR;
     double *X, *Y, *Z, *RX, *RZ;
     float4* OFF;
     float4* CLA;
@@ -252,6 +255,38 @@ __device__ __forceinline__ double serial_sub(double acc, double t, int gbase) {
     return acc;
 }
 
+// One symmetry pair exactly as Kernel.cu:305-310 computes it, for the reflected row pose
+// (rx, ry, rr) and object j's pose (xj, yj, ryj).
+__device__ __forceinline__ float sym_val_exact(float xj, float yj, double ryj, float rx, float ry,
+                                               double rr) {
+    const float dp = (float)distance_f(xj, yj, rx, ry);
+    float dt = (float)(ryj - rr);
+    if (dt > kPI) dt = (float)((double)dt - kTwoPI);
+    const float head = 5.0f - sqrtf(dp);
+    return (float)((double)head - 0.4 * (double)fabsf(dt));
+}
+
+// fp32 estimate of sym_val_exact from q = {xf, yf, rotYf, -}: exact float differences,
+// hardware (1 ulp) square roots, fp32 wrap and combine.
+__device__ __forceinline__ float sym_val_fast(float4 q, float rx, float ry, float rr) {
+    const float dx = q.x - rx;
+    const float dy = q.y - ry;
+    const float s = fmaf(dx, dx, dy * dy);
+    const float h = __builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf(s));
+    float dt = q.z - rr;
+    dt = (dt > 3.1416f) ? dt - 6.2832f : dt;
+    return fmaf(-0.4f, fabsf(dt), 5.0f - h);
+}
+
+// Bound on |sym_val_fast - sym_val_exact| for an estimate v in a row with reflected angle rr,
+// for poses with |x|, |y|, |rotY| < 1e15. Derivation (DESIGN.md "Symmetry estimate"): the
+// square-root chain contributes <= 2^-21 (5 + |v|), the rotation difference and wrap <= 2^-22
+// (12.6 + 2|v| + |rr|) x 0.4, the fp32 combine <= 2^-23 (15 + 2|v|) and the reference's own
+// final rounding 2^-24 |v|; together < 2^-21 (12 + 2.2|v| + 0.1|rr|). A 4x margin gives:
+__device__ __forceinline__ float sym_err(float v, float rr) {
+    return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
+}
+
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
@@ -266,6 +301,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     double px[NPL], py[NPL];
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
+    bool wild = false;  // a pose outside the range the fp32 symmetry estimate is proven for
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
@@ -276,12 +312,13 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             const ObjConst oc = a.objc[i];
             const ObjP p = ch.P[i];
             const double x = ch.X[i], y = ch.Y[i];
+            wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(ch.RY[i]) < 1e15);
             // VisualBalanceCosts products, Kernel.cu:200-201.
             px[m] = (double)oc.area * x;
             py[m] = (double)oc.area * y;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188.
             float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
-            float b = at - (float)p.rotY;
+            float b = at - p.rotYf;
             float ph = (float)((double)b + kHalfPI);
             cph[m] = cos_f32(ph);
             // SymmetryCosts row setup, Kernel.cu:292-299.
@@ -290,7 +327,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             float sd = (float)(2.0 * (rm.along_f - al));
             rxs[m] = (float)(x + (double)(sd * rm.ux));
             rys[m] = (float)(y + (double)(sd * rm.uy));
-            float rr = (float)(rm.two_focal_rot - p.rotY);
+            float rr = (float)(rm.two_focal_rot - ch.RY[i]);
             if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
             rrs[m] = rr;
             // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
@@ -308,42 +345,110 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     }
     wave_sync();
 
-    // Phase B: symmetry rows, Kernel.cu:301-312 (max is exact, so any j order works).
-    float rowmax[NPL];
+    // Phase B: symmetry rows, Kernel.cu:301-312. Row max over j of the reference's value,
+    // which needs two correctly rounded square roots and ~25 fp64 operations per pair.
+    // Scan every pair with an fp32 estimate whose error is bounded by sym_err(), keep the two
+    // largest estimates, and evaluate the reference's formula exactly for the leader. When
+    // the top two are closer than their error bounds (or a pose is outside the proven range)
+    // the row falls back to the exact value of every candidate within the bound. max is
+    // exact, so the result is the reference's bit for bit.
+    const bool exact_mode = group_ballot<L>(wild, gbase) != 0;
+    float rowmax[NPL], m1[NPL], m2[NPL];
+    int j1[NPL];
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        m1[m] = m2[m] = -INFINITY;
+        j1[m] = -1;
+    }
+#pragma unroll 2
+    for (int j = 0; j < n; ++j) {
+        const float4 q = *reinterpret_cast<const float4*>(&ch.P[j]);
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
+            const float v = sym_val_fast(q, rxs[m], rys[m], rrs[m]);
+            m2[m] = __builtin_amdgcn_fmed3f(m1[m], m2[m], v);
+            const bool up = v > m1[m];
+            m1[m] = up ? v : m1[m];
+            j1[m] = up ? j : j1[m];
+        }
+    }
+    bool amb[NPL];
+    bool any_amb = false;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
+        const bool row = i < n;
+        const bool clear = j1[m] >= 0 &&
+                           (m2[m] == -INFINITY ||
+                            m1[m] - m2[m] > sym_err(m1[m], rrs[m]) + sym_err(m2[m], rrs[m]));
+        amb[m] = row && (exact_mode || !clear);
+        any_amb |= amb[m];
         float best = 0.0f;
-        if (i < n) {
-            const float rx = rxs[m], ry = rys[m];
-            const double rr = (double)rrs[m];
-#pragma unroll 4
-            for (int j = 0; j < n; ++j) {
-                const ObjP q = ch.P[j];
-                float dp = (float)distance_f(q.xf, q.yf, rx, ry);
-                float dt = (float)(q.rotY - rr);
-                if (dt > kPI) dt = (float)((double)dt - kTwoPI);
-                float head = 5.0f - sqrtf(dp);
-                float val = (float)((double)head - 0.4 * (double)fabsf(dt));
-                best = fmaxf(best, val);
-            }
+        if (row && j1[m] >= 0) {
+            const ObjP q = ch.P[j1[m]];
+            best = fmaxf(0.0f, sym_val_exact(q.xf, q.yf, ch.RY[j1[m]], rxs[m], rys[m],
+                                             (double)rrs[m]));
         }
         rowmax[m] = best;
     }
+    if (__ballot(any_amb)) {
+        float thr[NPL], best[NPL];
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
+            thr[m] = (exact_mode || j1[m] < 0) ? INFINITY
+                                               : 2.0f * sym_err(fabsf(m1[m]) + 1.0f, rrs[m]);
+            best[m] = 0.0f;
+        }
+        for (int j = 0; j < n; ++j) {
+            const ObjP q = ch.P[j];
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) {
+                if (amb[m]) {
+                    const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rxs[m],
+                                                 rys[m], rrs[m]);
+                    if (!(v < m1[m] - thr[m]))
+                        best[m] = fmaxf(best[m], sym_val_exact(q.xf, q.yf, ch.RY[j], rxs[m],
+                                                               rys[m], (double)rrs[m]));
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < NPL; ++m)
+            if (amb[m]) rowmax[m] = best[m];
+    }
 
-    // Phase C: the object-ordered sums (VisualBalance nx/ny, FocalPoint, Symmetry).
-    float nx = 0.0f, ny = 0.0f, sym = 0.0f;
-    double fp = 0.0;
+    // Phase C: the object-ordered sums VisualBalance nx, ny (float, through double
+    // temporaries, :200-201), FocalPoint (double, :277) and Symmetry (float, :314). Lanes
+    // 0..3 of the group each replay one of the four sums in object order from LDS; every
+    // step is rn_d(acc + v), rounded on to float for the float accumulators (rn_f(rn_d(a - b))
+    // == rn_f(a - b) for floats a, b: double rounding is innocuous at 53 >= 2*24 + 2 bits).
+    double acc = 0.0;
+    const bool to_float = (r != 2);
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        if (m > 0) wave_sync();
+        if (i < n) {
+            double* row = ch.SCR + 4 * r;
+            row[0] = px[m];
+            row[1] = py[m];
+            row[2] = -(double)cph[m];
+            row[3] = -(double)rowmax[m];
+        }
+        wave_sync();
         const int cnt = min(L, n - m * L);
-        for (int l = 0; l < cnt; ++l) {
-            nx = (float)((double)nx + grp_get<L>(px[m], l, gbase));
-            ny = (float)((double)ny + grp_get<L>(py[m], l, gbase));
-            fp = fp - (double)grp_get<L>(cph[m], l, gbase);
-            sym = sym - grp_get<L>(rowmax[m], l, gbase);
+        if (r < 4) {
+            for (int l = 0; l < cnt; ++l) {
+                const double t = acc + ch.SCR[4 * l + r];
+                acc = to_float ? (double)(float)t : t;
+            }
         }
     }
+    const float nx = (float)grp_get<L>(acc, 0, gbase);
+    const float ny = (float)grp_get<L>(acc, 1, gbase);
+    const double fp = grp_get<L>(acc, 2, gbase);
+    const float sym = (float)grp_get<L>(acc, 3, gbase);
+    wave_sync();
     const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
 
     // Phase D: SurfaceAreaCosts, clearances first then objects (Kernel.cu:453-480).
@@ -383,7 +488,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 tpw = f * f;
             }
             const ObjP s1 = ch.P[rc.as], t1 = ch.P[rc.at];
-            const double th = theta_f(s1.xf, s1.yf, t1.xf, t1.yf, (float)t1.rotY);
+            const double th = theta_f(s1.xf, s1.yf, t1.xf, t1.yf, t1.rotYf);
             if (rc.amin > rc.amax) {
                 double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
                 float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
@@ -449,7 +554,7 @@ __device__ __forceinline__ Backup read_obj(const ChainPtrs& ch, int k) {
     b.y = ch.Y[k];
     b.z = ch.Z[k];
     b.rx = ch.RX[k];
-    b.ry = ch.P[k].rotY;
+    b.ry = ch.RY[k];
     b.rz = ch.RZ[k];
     return b;
 }
@@ -464,8 +569,10 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, 
     ObjP p;
     p.xf = (float)x;
     p.yf = (float)y;
-    p.rotY = ry;
+    p.rotYf = (float)ry;
+    p.pad = 0.0f;
     ch.P[k] = p;
+    ch.RY[k] = ry;
 }
 
 // Applies one proposal to the configuration in LDS; `writer` also records the overwritten
@@ -569,6 +676,8 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     unsigned char* base = lds + a.lay.hdr + (wave * G + g) * a.lay.stride;
     ChainPtrs ch;
     ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
+    ch.RY = reinterpret_cast<double*>(base + a.lay.RY);
+    ch.SCR = reinterpret_cast<double*>(base + a.lay.SCR);
     ch.X = reinterpret_cast<double*>(base + a.lay.X);
     ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
     ch.Z = reinterpret_cast<double*>(base + a.lay.Z);
@@ -593,8 +702,11 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         ObjP p;
         p.xf = (float)x;
         p.yf = (float)y;
-        p.rotY = src[F_RY * n + i];
+        const double ry = src[F_RY * n + i];
+        p.rotYf = (float)ry;
+        p.pad = 0.0f;
         ch.P[i] = p;
+        ch.RY[i] = ry;
     }
     wave_sync();
 
@@ -668,7 +780,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
                 p.y = (float)ch.Y[i];
                 p.z = (float)ch.Z[i];
                 p.rotX = (float)ch.RX[i];
-                p.rotY = (float)ch.P[i].rotY;
+                p.rotY = (float)ch.RY[i];
                 p.rotZ = (float)ch.RZ[i];
                 a.pts[chain * (int64_t)n + i] = p;
             }
@@ -682,7 +794,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
             dst[F_Y * n + i] = ch.Y[i];
             dst[F_Z * n + i] = ch.Z[i];
             dst[F_RX * n + i] = ch.RX[i];
-            dst[F_RY * n + i] = ch.P[i].rotY;
+            dst[F_RY * n + i] = ch.RY[i];
             dst[F_RZ * n + i] = ch.RZ[i];
         }
     }

@@ -87,12 +87,14 @@ enum { F_X = 0, F_Y = 1, F_Z = 2, F_RX = 3, F_RY = 4, F_RZ = 5, F_COUNT = 6 };
 // LDS carve-up. One workgroup = WAVES waves; each wave holds G = 64/L chains.
 struct ChainLds {
     int hdr;     // bytes of the per-workgroup header (frozen flags)
-    int P;       // ObjP[N]   {float xf, yf; double rotY}
+    int P;       // ObjP[N]   {float xf, yf, rotYf, pad}
+    int RY;      // double[N] rotY
     int X, Y;    // double[N]
     int Z, RX, RZ;
     int OFF;     // float4[N] off-limits boxes of the current configuration
     int CLA;     // float4[C] clearance boxes at their source objects
     int AUX;     // ChainAux: proposal backups and the current costs
+    int SCR;     // double[L][4] scratch of the ordered object sums
     int stride;  // bytes per chain
 };
 
@@ -103,6 +105,7 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int L) {
     l.hdr = round16(n + 1);
     int o = 0;
     l.P = o;   o += round16(16 * n);
+    l.RY = o;  o += round16(8 * n);
     l.X = o;   o += round16(8 * n);
     l.Y = o;   o += round16(8 * n);
     l.Z = o;   o += round16(8 * n);
@@ -111,7 +114,7 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int L) {
     l.OFF = o; o += round16(16 * n);
     l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
     l.AUX = o; o += 192;
-    (void)L;
+    l.SCR = o; o += 32 * L;
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
     l.stride = o;

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes written by tools/profile_box.sh.
+
+    python tools/pmc_summary.py gpurun_out/<tag> [--kernel SUBSTR] [--chains N] [--json OUT]
+
+Prints, per kernel (default: the chain step kernel), the per-dispatch mean of every counter
+collected, plus derived figures. HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so the
+read side is doubled (an upper bound for narrower accesses). --json writes the traffic record
+bench.py reads (profiles/pmc_step_kernel.json).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(tag_dir, kernel_substr):
+    per = defaultdict(list)  # counter -> values (one per dispatch)
+    meta = {}
+    for f in glob.glob(os.path.join(tag_dir, "pmc_*", "pmc_counter_collection.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel_substr not in row["Kernel_Name"]:
+                    continue
+                per[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                meta = {k: row[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size",
+                                            "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
+                                            "Scratch_Size")}
+                meta["duration_ns"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+    return {k: sum(v) / len(v) for k, v in per.items()}, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag_dir")
+    ap.add_argument("--kernel", default="mh_kernel<64, 1, 1>")
+    ap.add_argument("--chains", type=int, default=65536)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    c, meta = load(a.tag_dir, a.kernel)
+    if not c:
+        raise SystemExit(f"no dispatches of {a.kernel!r} under {a.tag_dir}")
+    print(json.dumps(meta))
+    for k in sorted(c):
+        print(f"{k:28s} {c[k]:.6g}")
+    d = {}
+    if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_VALU" in c:
+        d["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
+    if "SQ_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
+        d["sq_busy_frac"] = c["SQ_BUSY_CYCLES"] / c["GRBM_GUI_ACTIVE"]
+    if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
+        d["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+    if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+        rd = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024
+        wr = c.get("WRITE_SIZE", 0.0) * 1024
+        d["hbm_read_bytes_corrected"] = rd
+        d["hbm_write_bytes"] = wr
+        d["hbm_bytes_per_launch"] = rd + wr
+    for k, v in d.items():
+        print(f"{k:28s} {v:.6g}")
+    if a.json and "hbm_bytes_per_launch" in d:
+        rec = {"kernel": meta.get("Kernel_Name"), "chains_per_launch": a.chains,
+               "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
+               "fetch_size_kib": c.get("FETCH_SIZE"), "write_size_kib": c.get("WRITE_SIZE"),
+               "correction": "read side = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
+               "source": os.path.normpath(a.tag_dir)}
+        with open(a.json, "w") as fh:
+            json.dump(rec, fh, indent=1)
+        print("wrote", a.json)
+
+
+if __name__ == "__main__":
+    main()
