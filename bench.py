@@ -44,6 +44,34 @@ def state_bytes_per_chain(n: int) -> int:
     return 2 * (6 * 8 * n) + 2 * 64
 
 
+def shard(rank: int, chains_per_rank: int):
+    """Global chain ids [offset, offset + count) owned by `rank` (weak scaling: every rank owns
+    chains_per_rank chains). Chain c always draws Philox subsequence c, so a chain's result does
+    not depend on how many ranks there are."""
+    return rank * chains_per_rank, chains_per_rank
+
+
+def summary_record(sum_total: float, best_total: float, best_chain: int, n_chains: int,
+                   accepted: int):
+    """The per-rank record all-gathered over RCCL (40 bytes of payload as float64)."""
+    return [float(sum_total), float(best_total), float(best_chain), float(n_chains),
+            float(accepted)]
+
+
+def combine_records(recs):
+    """Combines all-gathered summary records (rows of summary_record) into the job result:
+    global best (lowest global chain id on ties), mean final cost, chain and accept counts."""
+    best = None
+    for r in recs:
+        key = (r[1], -r[2])
+        if best is None or key > (best[1], -best[2]):
+            best = r
+    total = sum(int(r[3]) for r in recs)
+    return {"best_final_cost": float(best[1]), "best_chain": int(best[2]),
+            "mean_final_cost": sum(r[0] for r in recs) / total, "chains": total,
+            "accepted": int(sum(r[4] for r in recs))}
+
+
 def cpu_baseline(room, orc, seed: int, budget_s: float, threads: int):
     """Oracle chain (the reference's algorithm, Kernel.cu:777-828, OffLimits included as the
     reference computes it every step) on `threads` host cores, bounded to ~budget_s."""
@@ -111,8 +139,8 @@ def main() -> int:
     torch.cuda.set_stream(stream)
     handle = stream.cuda_stream
     assert handle, "need a non-null HIP stream handle"
-    sess = mh.Session(room, args.chains, seed=args.seed, device=local_rank,
-                      chain_offset=rank * args.chains)
+    offset, count = shard(rank, args.chains)
+    sess = mh.Session(room, count, seed=args.seed, device=local_rank, chain_offset=offset)
     lanes, cpw = sess.geometry()
 
     for _ in range(args.warmup):
@@ -139,8 +167,8 @@ def main() -> int:
     sess.finalize(handle)
     torch.cuda.synchronize()
     s = sess.summary()
-    rec = torch.tensor([s.sum_total, float(s.best_total), float(s.best_chain),
-                        float(s.n_chains), float(s.accepted)], dtype=torch.float64,
+    rec = torch.tensor(summary_record(s.sum_total, s.best_total, s.best_chain, s.n_chains,
+                                      s.accepted), dtype=torch.float64,
                        device=f"cuda:{local_rank}")
     times = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
     if world > 1:
@@ -151,12 +179,10 @@ def main() -> int:
     else:
         recs = rec.unsqueeze(0).cpu()
     wall, kernel_ms = float(times[0]), float(times[1])
-    best_rank = int(torch.argmax(recs[:, 1]))
-    total_chains = int(recs[:, 3].sum())
-    mean_cost = float(recs[:, 0].sum()) / total_chains
-    best_cost = float(recs[best_rank, 1])
-    best_chain = int(recs[best_rank, 2])
-    accept_rate = float(recs[:, 4].sum()) / (total_chains * (args.warmup + args.steps) * args.iters)
+    job = combine_records(recs.tolist())
+    total_chains = job["chains"]
+    mean_cost, best_cost, best_chain = job["mean_final_cost"], job["best_final_cost"], job["best_chain"]
+    accept_rate = job["accepted"] / (total_chains * (args.warmup + args.steps) * args.iters)
 
     chain_steps = total_chains * args.steps * args.iters
     value = chain_steps / wall

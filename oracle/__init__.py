@@ -67,6 +67,10 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_run_chains.restype = C.c_int
     lib.orc_run_chains_state.argtypes = lib.orc_run_chains.argtypes
     lib.orc_run_chains_state.restype = C.c_int
+    lib.orc_rand_int.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.orc_rand_int.restype = C.c_int
+    lib.orc_pick_object.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    lib.orc_pick_object.restype = C.c_int
     lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.orc_accept.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.orc_accept.restype = C.c_int

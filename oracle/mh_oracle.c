@@ -412,11 +412,17 @@ static int rand_int(orc_rng* r, int max, int min) {
     return (int)truncf(u);
 }
 
+int orc_rand_int(orc_rng* r, int max, int min) { return rand_int(r, max, min); }
+
 /* Object pick with redraw while frozen (Kernel.cu:598-602); index nObjs is frozen. */
 static int pick_object(const positionAndRotation* cfg, int n, orc_rng* r) {
     int k = rand_int(r, n - 1, 0);
     while (k >= n || cfg[k].frozen) k = rand_int(r, n - 1, 0);
     return k;
+}
+
+int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r) {
+    return pick_object(cfg, n, r);
 }
 
 void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r) {

@@ -70,6 +70,11 @@ void orc_philox_stream(uint64_t seed, uint64_t subsequence, uint32_t* out, int n
 /* Random123 philox4x32 with 10 rounds on one (counter, key) block, for KAT vectors. */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
+/* generateRandomIntInRange (Kernel.cu:566-574) and the object pick with its frozen redraw
+ * (Kernel.cu:598-602; index nObjs counts as frozen). */
+int orc_rand_int(orc_rng* r, int max, int min);
+int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r);
+
 /* One proposal (Kernel.cu:576-704) applied in place to cfg (nObjs entries). */
 void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r);
 /* Accept rule of Kernel.cu:706-713. */

@@ -1,0 +1,105 @@
+"""The C-ABI boundary without a GPU: wire-struct layout, exported symbols, the header compiling
+as C and C++, and the host-side validation paths of KernelWrapper (which return before any HIP
+call). Compute entry points are exercised by tests/test_gpu_parity.py on the MI355X."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "mh_kernel.h"
+
+
+def test_struct_layout_matches_reference(mh):
+    for cls, (size, offsets) in mh.STRUCT_LAYOUT.items():
+        assert C.sizeof(cls) == size, cls.__name__
+        for field, off in offsets.items():
+            assert getattr(cls, field).offset == off, (cls.__name__, field)
+
+
+def test_library_exports_every_declared_symbol(mh, hiplib):
+    declared = set(re.findall(r"MH_API\s+[\w\s\*]+?\b(\w+)\s*\(", HEADER.read_text()))
+    assert declared == set(mh.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", str(mh.LIB_PATH)], check=True,
+                         capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared <= exported, declared - exported
+    for name in declared:
+        assert hasattr(hiplib, name)
+
+
+def test_library_is_gfx950_code(mh):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", "-h",
+                          str(mh.LIB_PATH)], capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    if out.returncode != 0 or "gfx" not in text:
+        data = mh.LIB_PATH.read_bytes()
+        assert b"gfx950" in data
+    else:
+        assert "gfx950" in text
+
+
+@pytest.mark.parametrize("lang,compiler", [("c", "gcc"), ("c++", "g++")])
+def test_header_compiles_and_links(mh, tmp_path, lang, compiler):
+    src = tmp_path / ("t.c" if lang == "c" else "t.cpp")
+    src.write_text("""
+#include "mh_kernel.h"
+#include <stdio.h>
+int main(void) {
+    result* (*kw)(relationshipStruct*, relationshipAngleStruct*, positionAndRotation*,
+                  rectangle*, rectangle*, vertex*, vertex*, Surface*, gpuConfig*) = KernelWrapper;
+    printf("%d %d %p\\n", (int)sizeof(result), (int)sizeof(Surface), (void*)kw);
+    KernelFreeResult(0);
+    return 0;
+}
+""")
+    exe = tmp_path / "t"
+    subprocess.run([compiler, "-std=c11" if lang == "c" else "-std=c++17", "-Wall", "-Werror",
+                    "-I", str(ROOT / "include"), str(src), "-o", str(exe),
+                    str(mh.LIB_PATH), f"-Wl,-rpath,{mh.LIB_PATH.parent}"], check=True)
+
+
+def _call(hiplib, mh, room, chains=4, iters=10):
+    g = mh.abi.gpuConfig(chains, 0, 64, 0, 0, iters)
+    return hiplib.KernelWrapperSeeded(*room.args(), C.byref(g), C.c_uint64(1))
+
+
+@pytest.mark.parametrize("breaker,needle", [
+    (lambda r: setattr(r.srf, "nObjs", 0), "nObjs"),
+    (lambda r: setattr(r.srf, "nClearances", 40), "nClearances"),
+    (lambda r: setattr(r.rss[0], "TargetIndex", 99), "relationship"),
+    (lambda r: setattr(r.clearances[1], "SourceIndex", -1), "SourceIndex"),
+    (lambda r: setattr(r.offlimits[3], "point1Index", 500), "point1Index"),
+])
+def test_invalid_rooms_return_null_with_message(mh, hiplib, breaker, needle):
+    room = mh.main_fixture()
+    breaker(room)
+    assert not _call(hiplib, mh, room)
+    assert needle in mh.last_error(hiplib)
+
+
+def test_all_frozen_is_an_error_not_a_hang(mh, hiplib):
+    room = mh.synthetic_room(8, freeze_every=1)
+    assert not _call(hiplib, mh, room)
+    assert "frozen" in mh.last_error(hiplib)
+
+
+def test_bad_gpu_config(mh, hiplib):
+    room = mh.main_fixture()
+    assert not _call(hiplib, mh, room, chains=0)
+    assert "gridxDim" in mh.last_error(hiplib)
+    assert not _call(hiplib, mh, room, iters=-1)
+    assert "iterations" in mh.last_error(hiplib)
+
+
+def test_null_arguments(mh, hiplib):
+    room = mh.main_fixture()
+    g = mh.abi.gpuConfig(1, 0, 64, 0, 0, 1)
+    args = list(room.args())
+    args[7] = None  # srf
+    assert not hiplib.KernelWrapper(*args, C.byref(g))
+    assert "srf" in mh.last_error(hiplib)
+    assert not hiplib.KernelWrapper(*room.args(), None)
+    hiplib.KernelFreeResult(None)

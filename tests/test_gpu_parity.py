@@ -211,3 +211,33 @@ def test_full_size_config3_properties(mh, orc, hiplib):
         rp, rc, _ = orc.run_chains(room, 1, steps, seed, chain_begin=cid)
         assert np.array_equal(pts[cid].view(np.uint32), rp[0].view(np.uint32)), cid
         assert np.array_equal(costs[cid].view(np.uint32), rc[0].view(np.uint32)), cid
+
+
+def _golden():
+    import importlib.util
+    import json
+    from pathlib import Path
+    d = Path(__file__).parent / "golden"
+    spec = importlib.util.spec_from_file_location("make_golden", d / "make_golden.py")
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return json.loads((d / "golden.json").read_text()), mg
+
+
+GOLDEN, MAKE_GOLDEN = _golden()
+
+
+@pytest.mark.parametrize("case", GOLDEN["chains"], ids=lambda c: f"{c['room']}{c['n']}")
+def test_golden_chains_hip(mh, hiplib, case):
+    room = MAKE_GOLDEN.make_room(mh, case)
+    pts, costs = mh.kernel_wrapper(room, case["chains"], case["steps"], seed=case["seed"])
+    assert MAKE_GOLDEN.sha(pts) == case["points_sha256"]
+    assert MAKE_GOLDEN.sha(costs) == case["costs_sha256"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["rng"], ids=lambda c: f"{c['seed']}-{c['subsequence']}")
+def test_golden_rng_hip(mh, hiplib, case):
+    u, f, g = mh.debug_rng(case["seed"], case["subsequence"], 16)
+    assert [int(x) for x in u] == case["u32"]
+    assert [int(x) for x in f.view(np.uint32)] == case["uniform_bits"]
+    assert [int(x) for x in g.view(np.uint32)] == case["normal_bits"]
