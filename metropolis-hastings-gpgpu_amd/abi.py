@@ -124,7 +124,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("MH_LIB", LIB_PATH))
     if not p.exists():
         raise MHError(f"{p} not found: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(str(p))

@@ -209,14 +209,14 @@ struct Geometry {
     mh::ChainLds lay;
 };
 
-bool choose_geometry(int n, int c, int device, Geometry& g) {
+bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     g.L = mh::choose_lanes(n);
     g.npl = mh::choose_npl(n, g.L);
     if (g.npl > mh::max_npl()) {
         set_error("nObjs too large (max " + std::to_string(64 * mh::max_npl()) + ")");
         return false;
     }
-    g.lay = mh::make_lds_layout(n, c, g.L);
+    g.lay = mh::make_lds_layout(n, c, r, g.L);
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
         max_lds = 64 * 1024;
@@ -307,7 +307,7 @@ bool upload(T** dst, const std::vector<T>& src, hipStream_t st) {
 bool session_init(mh_session* s) {
     MH_TRY_HIP(hipSetDevice(s->device));
     MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->device, s->geo)) return false;
+    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->geo)) return false;
     if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
     if (!upload(&s->d_rel, s->room.rel, s->stream)) return false;

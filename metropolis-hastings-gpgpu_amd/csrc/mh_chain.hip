@@ -22,8 +22,30 @@
 #include <rocrand/rocrand_uniform.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mh_launch.h"
+
+#ifndef MH_ABLATE
+#define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
+#endif
+#ifndef MH_DOUBLE
+#define MH_DOUBLE 0  // cost-probe builds: run phase k twice when bit k is set; product = 0
+#endif
+#define MH_REPS(bit) ((MH_DOUBLE & (bit)) ? 2 : 1)
+#define MH_CLOBBER() asm volatile("" ::: "memory")
+#ifndef MH_STAMPS
+#define MH_STAMPS 0  // diagnostic builds (tools/build_stamps.sh) time each phase; product = 0
+#endif
+
+#if MH_STAMPS
+__device__ unsigned long long g_phase_cycles[16];
+#define MH_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define MH_PHASE(ch, k, t0) do { unsigned long long _t; MH_STAMP(_t); (ch).aux->cyc[k] += _t - (t0); (t0) = _t; } while (0)
+#else
+#define MH_STAMP(t) do { } while (0)
+#define MH_PHASE(ch, k, t0) do { } while (0)
+#endif
 
 namespace mh {
 
@@ -33,24 +55,37 @@ struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds
     float pad;
 };
 
-struct Backup {
+struct Backup {  // the cost-relevant pose of one object (z, rotX, rotZ never enter a cost)
     int k;
-    double x, y, z, rx, ry, rz;
+    double x, y, ry;
 };
 
 // Per-chain scalars kept in LDS rather than registers while the costs are evaluated.
 struct ChainAux {
     Backup b[2];
     int nb;       // backups in use (0, 1 or 2)
+    int swap_a, swap_b;  // a swap proposal's objects (-1: none); z/rotX/rotZ swap in HBM on accept
     float cur[8]; // resultCosts of the current configuration
+#if MH_STAMPS
+    unsigned long long cyc[8];  // diagnostic: cycles per phase (writer lane)
+#endif
 };
-static_assert(sizeof(ChainAux) <= 192, "ChainAux");
+static_assert(sizeof(ChainAux) <= 256, "ChainAux");
 
 struct ChainPtrs {
+    const ObjConst* objc;  // room tables, staged once per workgroup into LDS
+    const ClrConst* clrc;
+    const RelConst* relc;
     ObjP* P;
     double* RY;
-    double* SCR;
-    double *X, *Y, *Z, *RX, *RZ;
+    double* OSD;      // [N][2] per-object double terms of the dense ordered sums (px, py)
+    float* OSF;       // [N][2] per-object float terms (-cos phi, -row max)
+    float* LCL;       // compacted non-zero Clearance terms (floats), capacity 2L
+    double* LPW;      // compacted non-zero PairWise / Angle terms, capacity lst_r each
+    double* LANG;
+    int lst_r;
+    double *X, *Y;
+    double* zrr;      // HBM: this chain's z, rotX, rotZ rows (F_Z, F_RX, F_RZ of the pose block)
     float4* OFF;
     float4* CLA;
     ChainAux* aux;
@@ -103,6 +138,7 @@ __device__ __forceinline__ double grp_get(double v, int src, int gbase) {
 // Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
 // OCML log/sin/cos code is not duplicated at every call site.
 __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
+    if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
     const double u1 = (double)a * 0x1p-32 + 0x1p-33;
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
     const double rad = sqrt(-2.0 * log(u1));
@@ -287,6 +323,37 @@ __device__ __forceinline__ float sym_err(float v, float rr) {
     return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
 }
 
+// ---- compacted term lists for the ordered sums -------------------------------------------
+//
+// Clearance terms (floats, capacity 2L) and PairWise / Angle terms (doubles, capacity lst_r =
+// min(L, R) each) are compacted in the reference's order into LDS lists. Lane 4 (Clearance),
+// 6 (PairWise) and 7 (Angle) of the group own those sums; a list that would overflow is first
+// folded into its owner's accumulator (only for pathologically overlapping rooms).
+
+template <typename T>
+__device__ __forceinline__ void list_flush(const T* buf, int& cnt, double& acc, bool owner,
+                                           bool to_float) {
+    wave_sync();
+    if (owner) {
+        for (int l = 0; l < cnt; ++l) {
+            const double t = acc + (double)buf[l];
+            acc = to_float ? (double)(float)t : t;
+        }
+    }
+    cnt = 0;
+    wave_sync();
+}
+
+// Appends, in lane order, the value of every lane whose `nz` is set.
+template <int L, typename T>
+__device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& acc, bool owner,
+                                            bool to_float, T v, bool nz, int r, int gbase) {
+    if (cnt + L > cap) list_flush(buf, cnt, acc, owner, to_float);
+    const uint64_t b = group_ballot<L>(nz, gbase);
+    if (nz) buf[cnt + __builtin_popcountll(b & ((1ull << r) - 1ull))] = v;
+    cnt += __builtin_popcountll(b);
+}
+
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
@@ -297,11 +364,15 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     const DevRoom& rm = a.rm;
     const int n = rm.n, c = rm.c;
 
+    unsigned long long t0 = 0;
+    MH_STAMP(t0);
     // Phase A: per-object and per-clearance terms of the owned slots.
     double px[NPL], py[NPL];
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
     bool wild = false;  // a pose outside the range the fp32 symmetry estimate is proven for
+    for (int rep = 0; rep < MH_REPS(1); ++rep) {
+    MH_CLOBBER();
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
@@ -309,7 +380,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
         sao[m] = sac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n) {
-            const ObjConst oc = a.objc[i];
+            const ObjConst oc = ch.objc[i];
             const ObjP p = ch.P[i];
             const double x = ch.X[i], y = ch.Y[i];
             wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(ch.RY[i]) < 1e15);
@@ -317,10 +388,12 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             px[m] = (double)oc.area * x;
             py[m] = (double)oc.area * y;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188.
-            float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
-            float b = at - p.rotYf;
-            float ph = (float)((double)b + kHalfPI);
-            cph[m] = cos_f32(ph);
+            if (!(MH_ABLATE & 2)) {
+                float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
+                float b = at - p.rotYf;
+                float ph = (float)((double)b + kHalfPI);
+                cph[m] = cos_f32(ph);
+            }
             // SymmetryCosts row setup, Kernel.cu:292-299.
             double al = x * (double)rm.ux;
             al = al + y * (double)rm.uy;
@@ -336,12 +409,13 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             sao[m] = comp_overlaps(rm, box);
         }
         if (i < c) {
-            const ClrConst cc = a.clrc[i];
+            const ClrConst cc = ch.clrc[i];
             const ObjP ps = ch.P[cc.src];
             ch.CLA[i] = shape_box(cc.shape, ps.xf, ps.yf);       // ClearanceCosts, :414-415
             const ObjP pi = ch.P[i];                              // SurfaceArea quirk: cfg[i], :456
             sac[m] = comp_overlaps(rm, shape_box(cc.shape, pi.xf, pi.yf));
         }
+    }
     }
     wave_sync();
 
@@ -352,16 +426,19 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // the top two are closer than their error bounds (or a pose is outside the proven range)
     // the row falls back to the exact value of every candidate within the bound. max is
     // exact, so the result is the reference's bit for bit.
+    if (r == 0) MH_PHASE(ch, 1, t0);
     const bool exact_mode = group_ballot<L>(wild, gbase) != 0;
     float rowmax[NPL], m1[NPL], m2[NPL];
     int j1[NPL];
+    for (int rep = 0; rep < MH_REPS(2); ++rep) {
+    MH_CLOBBER();
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         m1[m] = m2[m] = -INFINITY;
         j1[m] = -1;
     }
 #pragma unroll 2
-    for (int j = 0; j < n; ++j) {
+    for (int j = 0; j < ((MH_ABLATE & 1) ? 0 : n); ++j) {
         const float4 q = *reinterpret_cast<const float4*>(&ch.P[j]);
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
@@ -371,6 +448,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             m1[m] = up ? v : m1[m];
             j1[m] = up ? j : j1[m];
         }
+    }
     }
     bool amb[NPL];
     bool any_amb = false;
@@ -417,69 +495,72 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             if (amb[m]) rowmax[m] = best[m];
     }
 
-    // Phase C: the object-ordered sums VisualBalance nx, ny (float, through double
-    // temporaries, :200-201), FocalPoint (double, :277) and Symmetry (float, :314). Lanes
-    // 0..3 of the group each replay one of the four sums in object order from LDS; every
-    // step is rn_d(acc + v), rounded on to float for the float accumulators (rn_f(rn_d(a - b))
-    // == rn_f(a - b) for floats a, b: double rounding is innocuous at 53 >= 2*24 + 2 bits).
-    double acc = 0.0;
-    const bool to_float = (r != 2);
+    if (r == 0) MH_PHASE(ch, 2, t0);
+    // The eight ordered sums of Costs() -- VisualBalance nx and ny (float through double
+    // temporaries, :200-201), FocalPoint (double, :277), Symmetry (float, :314), SurfaceArea
+    // (float, :463-479), Clearance (float, :429), PairWise and PairWiseAngle (double, :222,
+    // :249/253) -- are replayed in the reference's order by lanes 0..7 of the group at once,
+    // from per-object values (dense) and compacted lists of the non-zero sparse terms
+    // (x - 0 == x, so dropping exact zeros is exact). Each step is rn_d(acc + v) with v the
+    // negated term where the reference subtracts, rounded on to float for the float
+    // accumulators (rn_f(rn_d(a + b)) == rn_f(a + b) for floats: 53 >= 2*24 + 2 bits).
+    if (r == 0) MH_PHASE(ch, 3, t0);
+    double acc = 0.0;  // lane k of the group owns sum k (k = 5 unused; SurfaceArea below)
+    const bool acc_float = (r == 0 || r == 1 || r == 3 || r == 4);
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
-        if (m > 0) wave_sync();
         if (i < n) {
-            double* row = ch.SCR + 4 * r;
-            row[0] = px[m];
-            row[1] = py[m];
-            row[2] = -(double)cph[m];
-            row[3] = -(double)rowmax[m];
-        }
-        wave_sync();
-        const int cnt = min(L, n - m * L);
-        if (r < 4) {
-            for (int l = 0; l < cnt; ++l) {
-                const double t = acc + ch.SCR[4 * l + r];
-                acc = to_float ? (double)(float)t : t;
-            }
+            ch.OSD[2 * i] = px[m];
+            ch.OSD[2 * i + 1] = py[m];
+            ch.OSF[2 * i] = -cph[m];
+            ch.OSF[2 * i + 1] = -rowmax[m];
         }
     }
-    const float nx = (float)grp_get<L>(acc, 0, gbase);
-    const float ny = (float)grp_get<L>(acc, 1, gbase);
-    const double fp = grp_get<L>(acc, 2, gbase);
-    const float sym = (float)grp_get<L>(acc, 3, gbase);
-    wave_sync();
-    const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
-
-    // Phase D: SurfaceAreaCosts, clearances first then objects (Kernel.cu:453-480).
+    // SurfaceAreaCosts: clearances (quirk box at cfg[i]) first, then objects (:453-480);
+    // its terms are almost always all zero, so the group walks the non-zero ones directly.
     float sa = 0.0f;
+    for (int rep = 0; rep < MH_REPS(4); ++rep) {
+    MH_CLOBBER();
+    sa = 0.0f;
 #pragma unroll
     for (int m = 0; m < NPL; ++m)
         if (m * L < c) sa = serial_sub4<L>(sa, sac[m], gbase);
 #pragma unroll
     for (int m = 0; m < NPL; ++m)
         if (m * L < n) sa = serial_sub4<L>(sa, sao[m], gbase);
+    }
 
-    // Phase E: ClearanceCosts, clearance-major, object-minor (Kernel.cu:408-431).
-    float cl = 0.0f;
-    for (int ci = 0; ci < c; ++ci) {
+    if (r == 0) MH_PHASE(ch, 4, t0);
+    // ClearanceCosts pairs, clearance-major then object (Kernel.cu:408-431).
+    int cnt_cl = 0;
+    for (int rep = 0; rep < MH_REPS(8); ++rep) {
+    MH_CLOBBER();
+    cnt_cl = 0;
+    for (int ci = 0; ci < ((MH_ABLATE & 8) ? 0 : c); ++ci) {
         const float4 A = ch.CLA[ci];
         for (int jb = 0; jb < n; jb += L) {
             const int j = jb + r;
             const float ar = (j < n) ? overlap(A, ch.OFF[j]) : 0.0f;
-            cl = serial_sub<L>(cl, ar, gbase);
+            list_append<L, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, -ar, ar != 0.0f, r,
+                                  gbase);
         }
     }
+    }
 
-    // Phase F: PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263).
-    double pw = 0.0, ang = 0.0;
-    for (int qb = 0; qb < rm.r; qb += L) {
+    if (r == 0) MH_PHASE(ch, 5, t0);
+    // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms.
+    int cnt_pw = 0, cnt_ang = 0;
+    for (int rep = 0; rep < MH_REPS(16); ++rep) {
+    MH_CLOBBER();
+    cnt_pw = cnt_ang = 0;
+    for (int qb = 0; qb < ((MH_ABLATE & 16) ? 0 : rm.r); qb += L) {
         const int q = qb + r;
         double tpw = 0.0, tang = 0.0;
         if (q < rm.r) {
-            const RelConst rc = a.relc[q];
-            const ObjP s0 = ch.P[rc.s], t0 = ch.P[rc.t];
-            const double d = distance_f(s0.xf, s0.yf, t0.xf, t0.yf);
+            const RelConst rc = ch.relc[q];
+            const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
+            const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
             if (d < rc.start) {
                 double f = d / rc.start;
                 tpw = f * f;
@@ -487,8 +568,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 double f = rc.end / d;
                 tpw = f * f;
             }
-            const ObjP s1 = ch.P[rc.as], t1 = ch.P[rc.at];
-            const double th = theta_f(s1.xf, s1.yf, t1.xf, t1.yf, t1.rotYf);
+            const ObjP as = ch.P[rc.as], at = ch.P[rc.at];
+            const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
             if (rc.amin > rc.amax) {
                 double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
                 float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
@@ -498,10 +579,67 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
             }
         }
-        pw = serial_sub<L>(pw, tpw, gbase);
-        ang = serial_sub<L>(ang, tang, gbase);
+        list_append<L, double>(ch.LPW, ch.lst_r, cnt_pw, acc, r == 6, false, -tpw, tpw != 0.0,
+                               r, gbase);
+        list_append<L, double>(ch.LANG, ch.lst_r, cnt_ang, acc, r == 7, false, -tang,
+                               tang != 0.0, r, gbase);
+    }
     }
 
+    // The replay: lane k walks its own sequence in the reference's order. Lanes 0/1: the
+    // VisualBalance products (double terms, float accumulators); 2: -cos phi (float terms,
+    // double accumulator); 3: -row max (float, float); 4: Clearance list (float, float);
+    // 6/7: PairWise / Angle lists (double, double).
+    wave_sync();
+    const double acc0 = acc;
+    for (int rep = 0; rep < MH_REPS(32); ++rep) {
+        MH_CLOBBER();
+        acc = acc0;
+        const int k = r;
+        int len = 0;
+        const double* dsrc = ch.OSD;
+        const float* fsrc = ch.OSF;
+        int dstride = 0, fstride = 0;
+        bool from_float = false;
+        if (k == 0 || k == 1) {
+            len = (MH_ABLATE & 4) ? 0 : n;
+            dsrc = ch.OSD + k;
+            dstride = 2;
+        } else if (k == 2 || k == 3) {
+            len = (MH_ABLATE & 4) ? 0 : n;
+            fsrc = ch.OSF + (k - 2);
+            fstride = 2;
+            from_float = true;
+        } else if (k == 4) {
+            len = cnt_cl;
+            fsrc = ch.LCL;
+            fstride = 1;
+            from_float = true;
+        } else if (k == 6 || k == 7) {
+            len = k == 6 ? cnt_pw : cnt_ang;
+            dsrc = k == 6 ? ch.LPW : ch.LANG;
+            dstride = 1;
+        }
+        const int steps = max(n, max(cnt_cl, max(cnt_pw, cnt_ang)));
+        for (int l = 0; l < steps; ++l) {
+            if (l < len) {
+                const double v = from_float ? (double)fsrc[l * fstride] : dsrc[l * dstride];
+                const double t = acc + v;
+                acc = acc_float ? (double)(float)t : t;
+            }
+        }
+    }
+    const float nx = (float)grp_get<L>(acc, 0, gbase);
+    const float ny = (float)grp_get<L>(acc, 1, gbase);
+    const double fp = grp_get<L>(acc, 2, gbase);
+    const float sym = (float)grp_get<L>(acc, 3, gbase);
+    const float cl = (float)grp_get<L>(acc, 4, gbase);
+    const double pw = grp_get<L>(acc, 6, gbase);
+    const double ang = grp_get<L>(acc, 7, gbase);
+    wave_sync();
+    const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
+
+    if (r == 0) MH_PHASE(ch, 6, t0);
     // OffLimitsCosts, pairs i < j (Kernel.cu:488-511): final / evaluation passes only.
     float ol = 0.0f;
     if constexpr (WITH_OL) {
@@ -552,20 +690,14 @@ __device__ __forceinline__ Backup read_obj(const ChainPtrs& ch, int k) {
     b.k = k;
     b.x = ch.X[k];
     b.y = ch.Y[k];
-    b.z = ch.Z[k];
-    b.rx = ch.RX[k];
     b.ry = ch.RY[k];
-    b.rz = ch.RZ[k];
     return b;
 }
 
-__device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, double y, double z,
-                                          double rx, double ry, double rz) {
+__device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, double y,
+                                          double ry) {
     ch.X[k] = x;
     ch.Y[k] = y;
-    ch.Z[k] = z;
-    ch.RX[k] = rx;
-    ch.RZ[k] = rz;
     ObjP p;
     p.xf = (float)x;
     p.yf = (float)y;
@@ -598,7 +730,8 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
         if (writer) {
             ch.aux->b[0] = b0;
             ch.aux->nb = 1;
-            write_obj(ch, k, x, y, b0.z, b0.rx, b0.ry, b0.rz);
+            ch.aux->swap_a = -1;
+            write_obj(ch, k, x, y, b0.ry);
         }
         return;
     }
@@ -613,13 +746,17 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
         if (writer) {
             ch.aux->b[0] = b0;
             ch.aux->nb = 1;
-            write_obj(ch, k, b0.x, b0.y, b0.z, b0.rx, ry, b0.rz);
+            ch.aux->swap_a = -1;
+            write_obj(ch, k, b0.x, b0.y, ry);
         }
         return;
     }
     // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
     if (n < 2) {
-        if (writer) ch.aux->nb = 0;
+        if (writer) {
+            ch.aux->nb = 0;
+            ch.aux->swap_a = -1;
+        }
         return;
     }
     const int ka = pick_object(rng, n, frozen);
@@ -630,9 +767,24 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
         ch.aux->b[0] = b0;
         ch.aux->b[1] = b1;
         ch.aux->nb = 2;
-        write_obj(ch, ka, b1.x, b1.y, b1.z, b1.rx, b1.ry, b1.rz);
-        write_obj(ch, kb, (double)(float)b0.x, (double)(float)b0.y, (double)(float)b0.z,
-                  (double)(float)b0.rx, (double)(float)b0.ry, (double)(float)b0.rz);
+        ch.aux->swap_a = ka;
+        ch.aux->swap_b = kb;
+        write_obj(ch, ka, b1.x, b1.y, b1.ry);
+        write_obj(ch, kb, (double)(float)b0.x, (double)(float)b0.y, (double)(float)b0.ry);
+    }
+}
+
+// An accepted swap also exchanges z, rotX and rotZ (Kernel.cu:675-700), which no cost reads:
+// they stay in HBM and are swapped there, object 1's values through float temporaries.
+__device__ __forceinline__ void commit_swap_zrr(const ChainPtrs& ch, int n) {
+    const int ka = ch.aux->swap_a, kb = ch.aux->swap_b;
+    if (ka < 0) return;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        double* row = ch.zrr + f * n;
+        const double va = row[ka], vb = row[kb];
+        row[ka] = vb;
+        row[kb] = (double)(float)va;
     }
 }
 
@@ -641,7 +793,7 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
     const int nb = ch.aux->nb;
     for (int q = nb - 1; q >= 0; --q) {
         const Backup b = ch.aux->b[q];
-        write_obj(ch, b.k, b.x, b.y, b.z, b.rx, b.ry, b.rz);
+        write_obj(ch, b.k, b.x, b.y, b.ry);
     }
 }
 
@@ -666,7 +818,14 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     const int gbase = g * L;
     const int waves_per_wg = blockDim.x >> 6;
 
-    unsigned char* frozen = lds;
+    // Room tables: staged once per workgroup (the chain loop then never touches global memory).
+    ObjConst* objc_l = reinterpret_cast<ObjConst*>(lds + a.lay.h_obj);
+    ClrConst* clrc_l = reinterpret_cast<ClrConst*>(lds + a.lay.h_clr);
+    RelConst* relc_l = reinterpret_cast<RelConst*>(lds + a.lay.h_rel);
+    unsigned char* frozen = lds + a.lay.h_frz;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) objc_l[i] = a.objc[i];
+    for (int i = threadIdx.x; i < a.rm.c; i += blockDim.x) clrc_l[i] = a.clrc[i];
+    for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) relc_l[i] = a.relc[i];
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     __syncthreads();
 
@@ -675,14 +834,20 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
 
     unsigned char* base = lds + a.lay.hdr + (wave * G + g) * a.lay.stride;
     ChainPtrs ch;
+    ch.objc = objc_l;
+    ch.clrc = clrc_l;
+    ch.relc = relc_l;
     ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
     ch.RY = reinterpret_cast<double*>(base + a.lay.RY);
-    ch.SCR = reinterpret_cast<double*>(base + a.lay.SCR);
+    ch.OSD = reinterpret_cast<double*>(base + a.lay.OSD);
+    ch.OSF = reinterpret_cast<float*>(base + a.lay.OSF);
+    ch.LCL = reinterpret_cast<float*>(base + a.lay.LCL);
+    ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
+    ch.lst_r = a.lay.lst_r;
+    ch.LANG = ch.LPW + ch.lst_r;
     ch.X = reinterpret_cast<double*>(base + a.lay.X);
     ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
-    ch.Z = reinterpret_cast<double*>(base + a.lay.Z);
-    ch.RX = reinterpret_cast<double*>(base + a.lay.RX);
-    ch.RZ = reinterpret_cast<double*>(base + a.lay.RZ);
+    ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
     ch.OFF = reinterpret_cast<float4*>(base + a.lay.OFF);
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
     ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
@@ -696,9 +861,11 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         const double x = src[F_X * n + i], y = src[F_Y * n + i];
         ch.X[i] = x;
         ch.Y[i] = y;
-        ch.Z[i] = src[F_Z * n + i];
-        ch.RX[i] = src[F_RX * n + i];
-        ch.RZ[i] = src[F_RZ * n + i];
+        if constexpr (OP == OP_INIT) {  // z, rotX, rotZ live in HBM only
+            ch.zrr[i] = src[F_Z * n + i];
+            ch.zrr[n + i] = src[F_RX * n + i];
+            ch.zrr[2 * n + i] = src[F_RZ * n + i];
+        }
         ObjP p;
         p.xf = (float)x;
         p.yf = (float)y;
@@ -734,21 +901,37 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         rng.bm_has = m0.bm_has;
         rng.bm_val = m0.bm_val;
         uint64_t accepted = m0.accepted;
+#if MH_STAMPS
+        if (writer)
+            for (int k = 0; k < 8; ++k) ch.aux->cyc[k] = 0;
+#endif
+#pragma clang loop unroll(disable)
         for (int it = 0; it < a.iterations; ++it) {
+            unsigned long long ts = 0;
+            MH_STAMP(ts);
             propose(rng, a.rm, frozen, ch, writer);
             wave_sync();
+            if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
             eval_costs<L, NPL, false>(a, ch, r, gbase, sc);
+            MH_STAMP(ts);
             if (accept(rng, sc[0], cur_total)) {
                 cur_total = sc[0];
                 ++accepted;
-                if (writer)
+                if (writer) {
                     for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
+                    commit_swap_zrr(ch, n);
+                }
             } else if (writer) {
                 restore(ch);
             }
             wave_sync();
+            if (writer) MH_PHASE(ch, 7, ts);
         }
+#if MH_STAMPS
+        if (writer)
+            for (int k = 0; k < 8; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
+#endif
         if (writer) {
             ChainMeta m;
             m.draws = rng.draws;
@@ -778,10 +961,10 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
                 point p;
                 p.x = (float)ch.X[i];
                 p.y = (float)ch.Y[i];
-                p.z = (float)ch.Z[i];
-                p.rotX = (float)ch.RX[i];
+                p.z = (float)ch.zrr[i];
+                p.rotX = (float)ch.zrr[n + i];
                 p.rotY = (float)ch.RY[i];
-                p.rotZ = (float)ch.RZ[i];
+                p.rotZ = (float)ch.zrr[2 * n + i];
                 a.pts[chain * (int64_t)n + i] = p;
             }
         }
@@ -792,10 +975,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         for (int i = r; i < n; i += L) {
             dst[F_X * n + i] = ch.X[i];
             dst[F_Y * n + i] = ch.Y[i];
-            dst[F_Z * n + i] = ch.Z[i];
-            dst[F_RX * n + i] = ch.RX[i];
             dst[F_RY * n + i] = ch.RY[i];
-            dst[F_RZ * n + i] = ch.RZ[i];
         }
     }
 }
@@ -897,6 +1077,11 @@ namespace mh {
 int choose_lanes(int n) {
     int L = 8;
     while (L < n && L < 64) L <<= 1;
+    if (const char* e = getenv("MH_LANES")) {  // tuning override: 8, 16, 32 or 64
+        const int want = atoi(e);
+        if ((want == 8 || want == 16 || want == 32 || want == 64) && (n + want - 1) / want <= 8)
+            L = want;
+    }
     return L;
 }
 int choose_npl(int n, int L) { return (n + L - 1) / L; }
@@ -908,18 +1093,28 @@ size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
 
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
+    // (lanes per chain, objects per lane) instantiations; npl rounds up to the next one.
     switch (L) {
-        case 8: return launch_geom<8, 1>(op, a, waves_per_wg, s);
-        case 16: return launch_geom<16, 1>(op, a, waves_per_wg, s);
-        case 32: return launch_geom<32, 1>(op, a, waves_per_wg, s);
-        default: break;
-    }
-    switch (npl) {
-        case 1: return launch_geom<64, 1>(op, a, waves_per_wg, s);
-        case 2: return launch_geom<64, 2>(op, a, waves_per_wg, s);
-        case 3:
-        case 4: return launch_geom<64, 4>(op, a, waves_per_wg, s);
-        default: return launch_geom<64, 8>(op, a, waves_per_wg, s);
+        case 8:
+            if (npl <= 1) return launch_geom<8, 1>(op, a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom<8, 2>(op, a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom<8, 4>(op, a, waves_per_wg, s);
+            return launch_geom<8, 8>(op, a, waves_per_wg, s);
+        case 16:
+            if (npl <= 1) return launch_geom<16, 1>(op, a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom<16, 2>(op, a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom<16, 4>(op, a, waves_per_wg, s);
+            return launch_geom<16, 8>(op, a, waves_per_wg, s);
+        case 32:
+            if (npl <= 1) return launch_geom<32, 1>(op, a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom<32, 2>(op, a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom<32, 4>(op, a, waves_per_wg, s);
+            return launch_geom<32, 8>(op, a, waves_per_wg, s);
+        default:
+            if (npl <= 1) return launch_geom<64, 1>(op, a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom<64, 2>(op, a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom<64, 4>(op, a, waves_per_wg, s);
+            return launch_geom<64, 8>(op, a, waves_per_wg, s);
     }
 }
 
@@ -928,6 +1123,14 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
     hipLaunchKernelGGL(mh_summary_kernel, dim3(1), dim3(1024), 0, s, costs, meta, n, chain_offset, out);
     return hipGetLastError();
 }
+
+#if MH_STAMPS
+extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 8) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
                       float* nrm, hipStream_t s) {

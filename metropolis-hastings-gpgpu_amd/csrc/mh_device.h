@@ -82,39 +82,55 @@ struct ChainMeta {
 static_assert(sizeof(ChainMeta) == 64, "ChainMeta");
 
 // Pose layout in HBM: chain-major, six SoA rows of N doubles.
-enum { F_X = 0, F_Y = 1, F_Z = 2, F_RX = 3, F_RY = 4, F_RZ = 5, F_COUNT = 6 };
+// x, y, rotY enter the costs; z, rotX, rotZ (contiguous, F_Z..F_RZ) never do.
+enum { F_X = 0, F_Y = 1, F_RY = 2, F_Z = 3, F_RX = 4, F_RZ = 5, F_COUNT = 6 };
 
 // LDS carve-up. One workgroup = WAVES waves; each wave holds G = 64/L chains.
 struct ChainLds {
-    int hdr;     // bytes of the per-workgroup header (frozen flags)
+    int hdr;     // bytes of the per-workgroup header: room tables + frozen flags
+    int h_obj;   // ObjConst[N] within the header
+    int h_clr;   // ClrConst[C]
+    int h_rel;   // RelConst[R]
+    int h_frz;   // unsigned char[N + 1] frozen flags (index N counts as frozen)
+    int h_room;  // DevRoom copy (read by the out-of-line cost evaluation)
     int P;       // ObjP[N]   {float xf, yf, rotYf, pad}
     int RY;      // double[N] rotY
-    int X, Y;    // double[N]
-    int Z, RX, RZ;
+    int X, Y;    // double[N]   (z, rotX, rotZ never enter a cost: they stay in HBM)
     int OFF;     // float4[N] off-limits boxes of the current configuration
     int CLA;     // float4[C] clearance boxes at their source objects
     int AUX;     // ChainAux: proposal backups and the current costs
-    int SCR;     // double[L][4] scratch of the ordered object sums
+    int OSD;     // double[N][2] per-object VisualBalance products of the ordered sums
+    int OSF;     // float[N][2]  per-object -cos(phi) and -row max
+    int LCL;     // float[2L]    compacted non-zero Clearance terms
+    int LPW;     // double[2 * lst_r] compacted non-zero PairWise then Angle terms
+    int lst_r;   // min(L, max(R, 1))
     int stride;  // bytes per chain
 };
 
 inline MH_HD int round16(int v) { return (v + 15) & ~15; }
 
-inline MH_HD ChainLds make_lds_layout(int n, int c, int L) {
+inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L) {
     ChainLds l;
-    l.hdr = round16(n + 1);
+    int h = 0;
+    l.h_obj = h; h += round16((int)sizeof(ObjConst) * n);
+    l.h_clr = h; h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
+    l.h_rel = h; h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
+    l.h_frz = h; h += round16(n + 1);
+    l.h_room = h; h += round16((int)sizeof(DevRoom));
+    l.hdr = h;
     int o = 0;
     l.P = o;   o += round16(16 * n);
     l.RY = o;  o += round16(8 * n);
     l.X = o;   o += round16(8 * n);
     l.Y = o;   o += round16(8 * n);
-    l.Z = o;   o += round16(8 * n);
-    l.RX = o;  o += round16(8 * n);
-    l.RZ = o;  o += round16(8 * n);
     l.OFF = o; o += round16(16 * n);
     l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
-    l.AUX = o; o += 192;
-    l.SCR = o; o += 32 * L;
+    l.AUX = o; o += 256;
+    l.lst_r = r < 1 ? 1 : (r < L ? r : L);
+    l.OSD = o; o += round16(16 * n);
+    l.OSF = o; o += round16(8 * n);
+    l.LCL = o; o += round16(8 * L);
+    l.LPW = o; o += round16(16 * l.lst_r);
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
     l.stride = o;

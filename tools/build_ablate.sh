@@ -1,0 +1,20 @@
+#!/bin/bash
+# Timing-only variants of libmhgpu.so with phases compiled out (MH_ABLATE bitmask):
+#   1 symmetry rows, 2 per-object atan2/cos, 4 ordered sums, 8 SurfaceArea/Clearance pairs,
+#   16 PairWise/Angle, 32 Box-Muller. Results are WRONG by construction; only time matters.
+# `stamps` builds the per-phase cycle-stamp diagnostic (tools/stamps.py) instead; `dblK`
+# runs phase bit K twice with identical results (cost probe: the trajectory is unchanged).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p ablate
+C=metropolis-hastings-gpgpu_amd/csrc
+for M in "$@"; do
+  case "$M" in
+    stamps) DEF=-DMH_STAMPS=1 ;;
+    dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
+    *) DEF=-DMH_ABLATE=$M ;;
+  esac
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
+    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
+done
+wait
