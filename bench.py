@@ -107,13 +107,14 @@ def pmc_traffic(n_chains_per_launch: int):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed launches")
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=99,
+                    help="timed launches (1 warmup + 99 = the config's 100k MH steps)")
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--iters", type=int, default=1000, help="MH steps per launch (<= 1000)")
     ap.add_argument("--objects", type=int, default=64)
     ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     args.iters = max(1, min(args.iters, 1000))

@@ -354,6 +354,32 @@ __device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& a
     cnt += __builtin_popcountll(b);
 }
 
+// PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
+__device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tpw, double& tang) {
+    tpw = 0.0;
+    tang = 0.0;
+    const RelConst rc = ch.relc[q];
+    const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
+    const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
+    if (d < rc.start) {
+        double f = d / rc.start;
+        tpw = f * f;
+    } else if (d > rc.end) {
+        double f = rc.end / d;
+        tpw = f * f;
+    }
+    const ObjP as = ch.P[rc.as], at = ch.P[rc.at];
+    const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
+    if (rc.amin > rc.amax) {
+        double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
+        float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
+        if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+    } else if (rc.amin < th || th < rc.amax) {
+        double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
+        tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+    }
+}
+
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
@@ -370,6 +396,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     double px[NPL], py[NPL];
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
+    double rpw[NPL], rang[NPL];  // relationship terms of chunks m < NPL (see Phase F)
     bool wild = false;  // a pose outside the range the fp32 symmetry estimate is proven for
     for (int rep = 0; rep < MH_REPS(1); ++rep) {
     MH_CLOBBER();
@@ -408,6 +435,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             ch.OFF[i] = box;
             sao[m] = comp_overlaps(rm, box);
         }
+        rpw[m] = rang[m] = 0.0;
+        if (!(MH_ABLATE & 16) && i < rm.r) rel_terms(ch, i, rpw[m], rang[m]);
         if (i < c) {
             const ClrConst cc = ch.clrc[i];
             const ObjP ps = ch.P[cc.src];
@@ -537,11 +566,16 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     for (int rep = 0; rep < MH_REPS(8); ++rep) {
     MH_CLOBBER();
     cnt_cl = 0;
+    float4 offb[NPL];
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) offb[m] = (m * L + r < n) ? ch.OFF[m * L + r] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int ci = 0; ci < ((MH_ABLATE & 8) ? 0 : c); ++ci) {
         const float4 A = ch.CLA[ci];
-        for (int jb = 0; jb < n; jb += L) {
-            const int j = jb + r;
-            const float ar = (j < n) ? overlap(A, ch.OFF[j]) : 0.0f;
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
+            if (m * L >= n) break;
+            const int j = m * L + r;
+            const float ar = (j < n) ? overlap(A, offb[m]) : 0.0f;
             list_append<L, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, -ar, ar != 0.0f, r,
                                   gbase);
         }
@@ -554,31 +588,18 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     for (int rep = 0; rep < MH_REPS(16); ++rep) {
     MH_CLOBBER();
     cnt_pw = cnt_ang = 0;
-    for (int qb = 0; qb < ((MH_ABLATE & 16) ? 0 : rm.r); qb += L) {
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        if (m * L >= rm.r) break;
+        list_append<L, double>(ch.LPW, ch.lst_r, cnt_pw, acc, r == 6, false, -rpw[m],
+                               rpw[m] != 0.0, r, gbase);
+        list_append<L, double>(ch.LANG, ch.lst_r, cnt_ang, acc, r == 7, false, -rang[m],
+                               rang[m] != 0.0, r, gbase);
+    }
+    for (int qb = NPL * L; qb < ((MH_ABLATE & 16) ? 0 : rm.r); qb += L) {  // R > L * NPL
         const int q = qb + r;
         double tpw = 0.0, tang = 0.0;
-        if (q < rm.r) {
-            const RelConst rc = ch.relc[q];
-            const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
-            const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
-            if (d < rc.start) {
-                double f = d / rc.start;
-                tpw = f * f;
-            } else if (d > rc.end) {
-                double f = rc.end / d;
-                tpw = f * f;
-            }
-            const ObjP as = ch.P[rc.as], at = ch.P[rc.at];
-            const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
-            if (rc.amin > rc.amax) {
-                double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
-                float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
-                if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
-            } else if (rc.amin < th || th < rc.amax) {
-                double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
-                tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
-            }
-        }
+        if (q < rm.r) rel_terms(ch, q, tpw, tang);
         list_append<L, double>(ch.LPW, ch.lst_r, cnt_pw, acc, r == 6, false, -tpw, tpw != 0.0,
                                r, gbase);
         list_append<L, double>(ch.LANG, ch.lst_r, cnt_ang, acc, r == 7, false, -tang,
@@ -621,10 +642,19 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             dstride = 1;
         }
         const int steps = max(n, max(cnt_cl, max(cnt_pw, cnt_ang)));
-        for (int l = 0; l < steps; ++l) {
-            if (l < len) {
-                const double v = from_float ? (double)fsrc[l * fstride] : dsrc[l * dstride];
-                const double t = acc + v;
+        // Terms past a lane's length read as +0 (acc + 0 == acc: an accumulator is never -0),
+        // so eight loads can be in flight ahead of the dependent adds.
+        for (int l0 = 0; l0 < steps; l0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int l = l0 + u;
+                v[u] = (l < len) ? (from_float ? (double)fsrc[l * fstride] : dsrc[l * dstride])
+                                 : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double t = acc + v[u];
                 acc = acc_float ? (double)(float)t : t;
             }
         }
