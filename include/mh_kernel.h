@@ -197,6 +197,11 @@ MH_API int mh_session_finalize(mh_session* s, void* stream);
 /* Synchronous copies of the finalised chains (either pointer may be NULL). */
 MH_API int mh_session_download(mh_session* s, point* out_points, resultCosts* out_costs);
 
+/* Synchronous copy of the costs each chain carries for its current state: the costs its last
+ * accepted proposal was judged by (OffLimitsCosts is 0: the step path does not evaluate it,
+ * Kernel.cu:548). Equal to a fresh evaluation of the state in every other field. */
+MH_API int mh_session_current_costs(mh_session* s, resultCosts* out_costs);
+
 /* Reduces the finalised chains on the device to one mh_summary (synchronous). */
 MH_API int mh_session_summary(mh_session* s, mh_summary* out);
 

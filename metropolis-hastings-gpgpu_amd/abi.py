@@ -106,7 +106,7 @@ COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointC
 # Every symbol include/mh_kernel.h declares.
 EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelFreeResult", "KernelLastError",
            "KernelEvaluateCosts", "mh_session_create", "mh_session_run", "mh_session_finalize",
-           "mh_session_download", "mh_session_summary", "mh_session_geometry",
+           "mh_session_download", "mh_session_current_costs", "mh_session_summary", "mh_session_geometry",
            "mh_session_destroy", "mh_debug_rng"]
 
 P = C.POINTER
@@ -151,6 +151,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_session_finalize.restype = C.c_int
     lib.mh_session_download.argtypes = [C.c_void_p, P(point), P(resultCosts)]
     lib.mh_session_download.restype = C.c_int
+    lib.mh_session_current_costs.argtypes = [C.c_void_p, P(resultCosts)]
+    lib.mh_session_current_costs.restype = C.c_int
     lib.mh_session_summary.argtypes = [C.c_void_p, P(mh_summary)]
     lib.mh_session_summary.restype = C.c_int
     lib.mh_session_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int)]
@@ -297,6 +299,14 @@ class Session:
             raise MHError(last_error(self.lib))
         p = np.frombuffer(bytes(pts), dtype=np.float32).reshape(self.chains, n, 6).copy()
         return p, costs_to_array(cs)
+
+    def current_costs(self) -> np.ndarray:
+        """Costs each chain carries for its current state (OffLimits 0), as the accept test saw
+        them."""
+        cs = (resultCosts * self.chains)()
+        if self.lib.mh_session_current_costs(self.h, cs) != 0:
+            raise MHError(last_error(self.lib))
+        return costs_to_array(cs)
 
     def summary(self) -> mh_summary:
         s = mh_summary()

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <float.h>
+#include <stddef.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -600,6 +601,20 @@ MH_API int mh_session_finalize(mh_session* s, void* stream) {
 MH_API int mh_session_download(mh_session* s, point* out_points, resultCosts* out_costs) {
     if (!s) { set_error("NULL session"); return -1; }
     return session_download(s, out_points, out_costs) ? 0 : -1;
+}
+
+MH_API int mh_session_current_costs(mh_session* s, resultCosts* out) {
+    if (!s || !out) { set_error("bad arguments"); return -1; }
+    if (hipSetDevice(s->device) != hipSuccess) { set_error("hipSetDevice failed"); return -1; }
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess && s->n_chains > 0)
+        e = hipMemcpy2D(out, sizeof(resultCosts), reinterpret_cast<const char*>(s->d_meta) + offsetof(mh::ChainMeta, costs),
+                        sizeof(mh::ChainMeta), sizeof(resultCosts), (size_t)s->n_chains, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        set_error(std::string("current costs: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
 }
 
 MH_API int mh_session_summary(mh_session* s, mh_summary* out) {

@@ -323,6 +323,52 @@ __device__ __forceinline__ float sym_err(float v, float rr) {
     return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
 }
 
+// Group-wide top two of (m1, m2) with the argmax of m1, butterfly over the group's lanes.
+template <int L>
+__device__ __forceinline__ void group_top2(float& m1, float& m2, int& j1) {
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) {
+        const float p1 = __shfl_xor(m1, off);
+        const float p2 = __shfl_xor(m2, off);
+        const int pj = __shfl_xor(j1, off);
+        const float lo = fminf(m1, p1);
+        const bool take = p1 > m1 || (p1 == m1 && pj < j1);  // ties: lowest index on every lane
+        m2 = fmaxf(lo, fmaxf(m2, p2));
+        m1 = fmaxf(m1, p1);
+        j1 = take ? pj : j1;
+    }
+}
+
+// Group-wide maximum of v with its index (ties: lowest index).
+template <int L>
+__device__ __forceinline__ void group_max_arg(float& v, int& j) {
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) {
+        const float pv = __shfl_xor(v, off);
+        const int pj = __shfl_xor(j, off);
+        const bool take = pv > v || (pv == v && pj < j);
+        v = take ? pv : v;
+        j = take ? pj : j;
+    }
+}
+
+// a[m] for a runtime m, as a select chain (no dynamic register indexing).
+template <int NPL, typename T>
+__device__ __forceinline__ T sel(const T (&a)[NPL], int m) {
+    T v = a[0];
+#pragma unroll
+    for (int q = 1; q < NPL; ++q) v = (m == q) ? a[q] : v;
+    return v;
+}
+
+// Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that
+// attains each (-1: the 0 floor of Kernel.cu:303 is the maximum).
+template <int NPL>
+struct SymRows {
+    float mx[NPL];
+    int arg[NPL];
+};
+
 // ---- compacted term lists for the ordered sums -------------------------------------------
 //
 // Clearance terms (floats, capacity 2L) and PairWise / Angle terms (doubles, capacity lst_r =
@@ -383,10 +429,14 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
-// {total, PW, VB, FP, SYM, CL, OL, SA}.
-template <int L, int NPL, bool WITH_OL>
+// {total, PW, VB, FP, SYM, CL, OL, SA}. `sym` returns the symmetry row maxima of the evaluated
+// configuration. With DELTA, `prev` holds them for the configuration before the proposal, which
+// differs from the evaluated one only in objects ka and kb (-1: none), and only the rows and
+// columns those objects touch are re-evaluated.
+template <int L, int NPL, bool WITH_OL, bool DELTA>
 __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
-                           float out[8]) {
+                           float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
+                           int kb) {
     const DevRoom& rm = a.rm;
     const int n = rm.n, c = rm.c;
 
@@ -450,14 +500,17 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
 
     // Phase B: symmetry rows, Kernel.cu:301-312. Row max over j of the reference's value,
     // which needs two correctly rounded square roots and ~25 fp64 operations per pair.
-    // Scan every pair with an fp32 estimate whose error is bounded by sym_err(), keep the two
-    // largest estimates, and evaluate the reference's formula exactly for the leader. When
-    // the top two are closer than their error bounds (or a pose is outside the proven range)
-    // the row falls back to the exact value of every candidate within the bound. max is
-    // exact, so the result is the reference's bit for bit.
+    // An fp32 estimate whose error is bounded by sym_err() screens the pairs; the reference's
+    // formula is evaluated exactly only where the estimate cannot rule a pair out, and max is
+    // exact, so the row maxima are the reference's bit for bit. A pose outside the range the
+    // bound is proven for (exact_mode) evaluates every pair exactly.
     if (r == 0) MH_PHASE(ch, 1, t0);
     const bool exact_mode = group_ballot<L>(wild, gbase) != 0;
-    float rowmax[NPL], m1[NPL], m2[NPL];
+    if constexpr (!DELTA) {
+    // Full scan: keep the two largest estimates per row and evaluate the leader exactly. When
+    // the top two are closer than their error bounds the row falls back to the exact value of
+    // every candidate within the bound.
+    float m1[NPL], m2[NPL];
     int j1[NPL];
     for (int rep = 0; rep < MH_REPS(2); ++rep) {
     MH_CLOBBER();
@@ -490,21 +543,24 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                             m1[m] - m2[m] > sym_err(m1[m], rrs[m]) + sym_err(m2[m], rrs[m]));
         amb[m] = row && (exact_mode || !clear);
         any_amb |= amb[m];
-        float best = 0.0f;
+        float e = 0.0f;
         if (row && j1[m] >= 0) {
             const ObjP q = ch.P[j1[m]];
-            best = fmaxf(0.0f, sym_val_exact(q.xf, q.yf, ch.RY[j1[m]], rxs[m], rys[m],
-                                             (double)rrs[m]));
+            e = sym_val_exact(q.xf, q.yf, ch.RY[j1[m]], rxs[m], rys[m], (double)rrs[m]);
         }
-        rowmax[m] = best;
+        sym.mx[m] = fmaxf(0.0f, e);
+        sym.arg[m] = e > 0.0f ? j1[m] : -1;
     }
     if (__ballot(any_amb)) {
-        float thr[NPL], best[NPL];
+        float thr[NPL];
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
             thr[m] = (exact_mode || j1[m] < 0) ? INFINITY
                                                : 2.0f * sym_err(fabsf(m1[m]) + 1.0f, rrs[m]);
-            best[m] = 0.0f;
+            if (amb[m]) {
+                sym.mx[m] = 0.0f;
+                sym.arg[m] = -1;
+            }
         }
         for (int j = 0; j < n; ++j) {
             const ObjP q = ch.P[j];
@@ -513,15 +569,152 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 if (amb[m]) {
                     const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rxs[m],
                                                  rys[m], rrs[m]);
-                    if (!(v < m1[m] - thr[m]))
-                        best[m] = fmaxf(best[m], sym_val_exact(q.xf, q.yf, ch.RY[j], rxs[m],
-                                                               rys[m], (double)rrs[m]));
+                    if (!(v < m1[m] - thr[m])) {
+                        const float e = sym_val_exact(q.xf, q.yf, ch.RY[j], rxs[m], rys[m],
+                                                      (double)rrs[m]);
+                        if (e > sym.mx[m]) {
+                            sym.mx[m] = e;
+                            sym.arg[m] = j;
+                        }
+                    }
                 }
             }
         }
+    }
+    } else {
+    // Delta: only rows ka, kb and columns ka, kb changed. An unchanged row keeps its maximum
+    // unless a changed column beats it (screened by the estimate) or its argmax column is a
+    // changed one whose value dropped; changed rows and such rows are re-scanned by the whole
+    // group, one row at a time.
+    bool need[NPL];
+    unsigned pend[NPL];
+    float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
+    if (ka >= 0) qa = *reinterpret_cast<const float4*>(&ch.P[ka]);
+    if (kb >= 0) qb = *reinterpret_cast<const float4*>(&ch.P[kb]);
+    bool any_pend = false;
 #pragma unroll
-        for (int m = 0; m < NPL; ++m)
-            if (amb[m]) rowmax[m] = best[m];
+    for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        const bool row = i < n;
+        const float cm = prev.mx[m];
+        const int ca = prev.arg[m];
+        sym.mx[m] = cm;
+        sym.arg[m] = ca;
+        need[m] = row && (i == ka || i == kb);
+        pend[m] = 0u;
+        if (row && !need[m]) {
+            if (ka >= 0) {
+                const float v = sym_val_fast(qa, rxs[m], rys[m], rrs[m]);
+                if (ca == ka || exact_mode || !(v + sym_err(v, rrs[m]) < cm)) pend[m] |= 1u;
+            }
+            if (kb >= 0) {
+                const float v = sym_val_fast(qb, rxs[m], rys[m], rrs[m]);
+                if (ca == kb || exact_mode || !(v + sym_err(v, rrs[m]) < cm)) pend[m] |= 2u;
+            }
+        }
+        any_pend |= pend[m] != 0u;
+    }
+    // Exact values of the pending (row, column) pairs: one evaluation site, each lane taking
+    // its lowest pending slot per pass.
+    while (__ballot(any_pend)) {
+        if (any_pend) {
+            int ms = NPL - 1;
+#pragma unroll
+            for (int m = NPL - 2; m >= 0; --m) ms = pend[m] ? m : ms;
+            const unsigned pm = sel<NPL>(pend, ms);
+            const int col = (pm & 1u) ? ka : kb;
+            const ObjP q = ch.P[col];
+            const float e = sym_val_exact(q.xf, q.yf, ch.RY[col], sel<NPL>(rxs, ms),
+                                          sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
+            any_pend = false;
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) {
+                if (m == ms) {
+                    pend[m] &= pend[m] - 1u;
+                    if (col == prev.arg[m] && !(e >= prev.mx[m])) {
+                        need[m] = true;  // the old maximum is gone: re-scan the row
+                    } else if (e > sym.mx[m]) {
+                        sym.mx[m] = e;
+                        sym.arg[m] = col;
+                    }
+                }
+                any_pend |= pend[m] != 0u;
+            }
+        }
+    }
+    // Re-scans, one row at a time across the whole group.
+    uint64_t rows[NPL];
+    bool any_row = false;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        rows[m] = group_ballot<L>(need[m], gbase);
+        any_row |= rows[m] != 0;
+    }
+    while (any_row) {
+        int ms = NPL - 1;
+#pragma unroll
+        for (int m = NPL - 2; m >= 0; --m) ms = rows[m] ? m : ms;
+        const uint64_t bm = sel<NPL>(rows, ms);
+        const int b = __builtin_ctzll(bm);
+        const float rx = grp_get<L>(sel<NPL>(rxs, ms), b, gbase);
+        const float ry = grp_get<L>(sel<NPL>(rys, ms), b, gbase);
+        const float rr = grp_get<L>(sel<NPL>(rrs, ms), b, gbase);
+        float t1 = -INFINITY, t2 = -INFINITY;
+        int tj = -1;
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) {
+            const int j = q * L + r;
+            if (j < n) {
+                const float v =
+                    sym_val_fast(*reinterpret_cast<const float4*>(&ch.P[j]), rx, ry, rr);
+                t2 = __builtin_amdgcn_fmed3f(t1, t2, v);
+                const bool up = v > t1;
+                t1 = up ? v : t1;
+                tj = up ? j : tj;
+            }
+        }
+        group_top2<L>(t1, t2, tj);
+        float best;
+        int barg;
+        if (!exact_mode && tj >= 0 &&
+            (t2 == -INFINITY || t1 - t2 > sym_err(t1, rr) + sym_err(t2, rr))) {
+            const ObjP q = ch.P[tj];
+            const float e = sym_val_exact(q.xf, q.yf, ch.RY[tj], rx, ry, (double)rr);
+            best = fmaxf(0.0f, e);
+            barg = e > 0.0f ? tj : -1;
+        } else {
+            const float thr =
+                (exact_mode || tj < 0) ? INFINITY : 2.0f * sym_err(fabsf(t1) + 1.0f, rr);
+            float bv = -INFINITY;
+            int bj = -1;
+            for (int j = r; j < n; j += L) {
+                const ObjP p = ch.P[j];
+                const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
+                if (!(v < t1 - thr)) {
+                    const float e = sym_val_exact(p.xf, p.yf, ch.RY[j], rx, ry, (double)rr);
+                    if (e > bv) {
+                        bv = e;
+                        bj = j;
+                    }
+                }
+            }
+            group_max_arg<L>(bv, bj);
+            best = bv > 0.0f ? bv : 0.0f;
+            barg = bv > 0.0f ? bj : -1;
+        }
+        any_row = false;
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
+            if (m == ms) {
+                if (r == b) {
+                    sym.mx[m] = best;
+                    sym.arg[m] = barg;
+                }
+                rows[m] &= rows[m] - 1;
+            }
+            any_row |= rows[m] != 0;
+        }
+    }
     }
 
     if (r == 0) MH_PHASE(ch, 2, t0);
@@ -543,7 +736,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             ch.OSD[2 * i] = px[m];
             ch.OSD[2 * i + 1] = py[m];
             ch.OSF[2 * i] = -cph[m];
-            ch.OSF[2 * i + 1] = -rowmax[m];
+            ch.OSF[2 * i + 1] = -sym.mx[m];
         }
     }
     // SurfaceAreaCosts: clearances (quirk box at cfg[i]) first, then objects (:453-480);
@@ -662,7 +855,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     const float nx = (float)grp_get<L>(acc, 0, gbase);
     const float ny = (float)grp_get<L>(acc, 1, gbase);
     const double fp = grp_get<L>(acc, 2, gbase);
-    const float sym = (float)grp_get<L>(acc, 3, gbase);
+    const float symc = (float)grp_get<L>(acc, 3, gbase);
     const float cl = (float)grp_get<L>(acc, 4, gbase);
     const double pw = grp_get<L>(acc, 6, gbase);
     const double ang = grp_get<L>(acc, 7, gbase);
@@ -688,7 +881,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     out[1] = rm.w_pw * pwc;
     out[2] = rm.w_vb * vb;
     out[3] = rm.w_fp * (float)fp;
-    out[4] = rm.w_sym * sym;
+    out[4] = rm.w_sym * symc;
     out[6] = rm.w_ol * ol;
     out[5] = rm.w_cl * cl;
     out[7] = rm.w_sa * sa;
@@ -738,8 +931,8 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, 
 }
 
 // Applies one proposal to the configuration in LDS; `writer` also records the overwritten
-// objects in ch.aux so a rejection can undo them.
-__device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* frozen,
+// objects in ch.aux so a rejection can undo them. Returns the objects it changed (-1: none).
+__device__ int2 propose(ChainRng& rng, const DevRoom& rm, const unsigned char* frozen,
                         const ChainPtrs& ch, bool writer) {
     const int n = rm.n;
     const int mode = rand_int(rng, 2, 0);
@@ -763,7 +956,7 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
             ch.aux->swap_a = -1;
             write_obj(ch, k, x, y, b0.ry);
         }
-        return;
+        return make_int2(k, -1);
     }
     if (mode == 1) {  // rotate, Kernel.cu:634-653
         const int k = pick_object(rng, n, frozen);
@@ -779,7 +972,7 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
             ch.aux->swap_a = -1;
             write_obj(ch, k, b0.x, b0.y, ry);
         }
-        return;
+        return make_int2(k, -1);
     }
     // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
     if (n < 2) {
@@ -787,7 +980,7 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
             ch.aux->nb = 0;
             ch.aux->swap_a = -1;
         }
-        return;
+        return make_int2(-1, -1);
     }
     const int ka = pick_object(rng, n, frozen);
     const int kb = pick_object(rng, n, frozen);
@@ -802,6 +995,7 @@ __device__ void propose(ChainRng& rng, const DevRoom& rm, const unsigned char* f
         write_obj(ch, ka, b1.x, b1.y, b1.ry);
         write_obj(ch, kb, (double)(float)b0.x, (double)(float)b0.y, (double)(float)b0.ry);
     }
+    return make_int2(ka, kb == ka ? -1 : kb);
 }
 
 // An accepted swap also exchanges z, rotX and rotZ (Kernel.cu:675-700), which no cost reads:
@@ -908,8 +1102,9 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     wave_sync();
 
     float cur[8];
+    SymRows<NPL> sym;  // symmetry row maxima of the current configuration
     if constexpr (OP == OP_INIT) {
-        eval_costs<L, NPL, false>(a, ch, r, gbase, cur);
+        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
         if (r == 0) {
             ChainMeta m;
             m.draws = 0;
@@ -931,6 +1126,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         rng.bm_has = m0.bm_has;
         rng.bm_val = m0.bm_val;
         uint64_t accepted = m0.accepted;
+        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 8; ++k) ch.aux->cyc[k] = 0;
@@ -939,14 +1135,16 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
         for (int it = 0; it < a.iterations; ++it) {
             unsigned long long ts = 0;
             MH_STAMP(ts);
-            propose(rng, a.rm, frozen, ch, writer);
+            const int2 kk = propose(rng, a.rm, frozen, ch, writer);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
-            eval_costs<L, NPL, false>(a, ch, r, gbase, sc);
+            SymRows<NPL> ss;
+            eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y);
             MH_STAMP(ts);
             if (accept(rng, sc[0], cur_total)) {
                 cur_total = sc[0];
+                sym = ss;
                 ++accepted;
                 if (writer) {
                     for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
@@ -973,7 +1171,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
             a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
-        eval_costs<L, NPL, true>(a, ch, r, gbase, cur);
+        eval_costs<L, NPL, true, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
         if (r == 0) {
             resultCosts rc;
             rc.totalCosts = cur[0];

@@ -117,6 +117,8 @@ def test_costs_match_oracle(mh, orc, hiplib, kind, n):
     ("syn", 5, 64, 200),
     ("syn", 1, 32, 50),          # swap with nObjs < 2 draws nothing more (Kernel.cu:657)
     ("syn", 64, 64, 150),        # config 3's room
+    ("syn", 64, 192, 1500),      # long chains: the cached symmetry row maxima over many accepts
+    ("syn", 20, 512, 2000),      # L = 32, two chains per wave
     ("syn", 100, 16, 60),        # NPL = 2
     ("syn", 256, 8, 25),         # config 5's room
 ])
@@ -211,6 +213,26 @@ def test_full_size_config3_properties(mh, orc, hiplib):
         rp, rc, _ = orc.run_chains(room, 1, steps, seed, chain_begin=cid)
         assert np.array_equal(pts[cid].view(np.uint32), rp[0].view(np.uint32)), cid
         assert np.array_equal(costs[cid].view(np.uint32), rc[0].view(np.uint32)), cid
+
+
+@pytest.mark.parametrize("n,chains,steps", [(64, 65536, 400), (20, 16384, 1500),
+                                             (256, 8192, 200), (5, 4096, 3000)])
+def test_running_costs_equal_fresh_evaluation(mh, hiplib, n, chains, steps):
+    """Size-independent property of the incremental evaluation: after many accepted proposals,
+    the costs every chain carries for its current state (symmetry row maxima updated
+    incrementally) equal a full re-evaluation of that state, bit for bit, on every chain."""
+    room = mh.synthetic_room(n)
+    with mh.Session(room, chains, seed=77 + n) as s:
+        s.run(steps)
+        s.finalize()
+        _, fresh = s.download()
+        running = s.current_costs()
+        acc = s.summary().accepted
+    assert acc > chains * steps // 20
+    keep = [0, 1, 2, 3, 4, 5, 7]  # all but OffLimits, which the step path does not evaluate
+    same = np.all(running[:, keep].view(np.uint32) == fresh[:, keep].view(np.uint32), axis=1)
+    assert same.all(), f"{(~same).sum()} of {chains} chains drifted"
+    assert np.all(running[:, 6] == 0)
 
 
 def _golden():
