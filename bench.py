@@ -142,7 +142,7 @@ def main() -> int:
     assert handle, "need a non-null HIP stream handle"
     offset, count = shard(rank, args.chains)
     sess = mh.Session(room, count, seed=args.seed, device=local_rank, chain_offset=offset)
-    lanes, cpw = sess.geometry()
+    lanes, cpw, step_kernel = sess.step_kernel()
 
     for _ in range(args.warmup):
         sess.run(args.iters, handle)
@@ -214,13 +214,15 @@ def main() -> int:
             "dtype": "f64+f32 (reference precision map)",
             "data": "synthetic (SURVEY.md 8(d) room, splitmix64 seed 0x5EED0000+N)",
             "config": {
-                "workload": f"config 3: {n}-object synthetic room, {args.chains} chains per GPU,"
+                "workload": ("config 3: " if (n, args.chains) == (64, 65536) else "")
+                            + f"{n}-object synthetic room, {args.chains} chains per GPU,"
                             f" {args.iters} MH steps per launch",
                 "objects": n, "clearances": c, "relationships": r,
                 "chains_per_gpu": args.chains, "global_chains": total_chains,
                 "mh_steps_per_step": args.iters,
                 "mh_steps_total": (args.warmup + args.steps) * args.iters,
                 "lanes_per_chain": lanes, "chains_per_workgroup": cpw,
+                "step_kernel": step_kernel,
                 "parallelism": f"chain-sharded x{world} (RCCL best-cost all-gather)",
             },
             "mean_final_cost": mean_cost,

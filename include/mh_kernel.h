@@ -205,9 +205,11 @@ MH_API int mh_session_current_costs(mh_session* s, resultCosts* out_costs);
 /* Reduces the finalised chains on the device to one mh_summary (synchronous). */
 MH_API int mh_session_summary(mh_session* s, mh_summary* out);
 
-/* Lanes per chain and chains per 256-thread workgroup the session's kernel uses. */
+/* Shape of the session's step kernel: lanes per chain, chains per workgroup, and whether it is
+ * the incremental-evaluation kernel (1) or the full-evaluation kernel (0). Any pointer may be
+ * NULL. */
 MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain,
-                               int* chains_per_workgroup);
+                               int* chains_per_workgroup, int* incremental);
 
 MH_API void mh_session_destroy(mh_session* s);
 
@@ -216,6 +218,11 @@ MH_API void mh_session_destroy(mh_session* s);
 /* The first n Philox words, uniforms (curand_uniform stand-in) and normals (curand_normal
  * stand-in) that chain `subsequence` draws under `seed`, computed on the current device by the
  * same device code the chains use (each stream restarted at draw 0). Returns 0 on success. */
+/* The group collectives the kernels use (top-2 / max-with-index / exclusive scan / max / sum
+ * over groups of L = 8, 16, 32 or 64 lanes), run on the current device for the 64 lane values
+ * v (floats) and iv (ints); out receives 9 x 64 ints (layout in mh_chain.hip). Returns 0. */
+MH_API int mh_debug_collectives(int L, const float* v, const int* iv, int* out);
+
 MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
                         float* out_uniform, float* out_normal);
 

@@ -7,5 +7,6 @@ bench use. The directory name contains hyphens, so load it with load_package() b
 importlib) rather than a plain import.
 """
 from .abi import (COST_FIELDS, EXPORTS, LIB_PATH, MHError, Room, Session, STRUCT_LAYOUT,  # noqa: F401
-                  debug_rng, evaluate_costs, kernel_wrapper, last_error, load_library)
+                  debug_collectives, debug_rng, evaluate_costs, kernel_wrapper, last_error,
+                  load_library)
 from .rooms import clone_cfg, main_fixture, synthetic_room  # noqa: F401

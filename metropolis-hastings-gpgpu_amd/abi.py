@@ -107,7 +107,7 @@ COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointC
 EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelFreeResult", "KernelLastError",
            "KernelEvaluateCosts", "mh_session_create", "mh_session_run", "mh_session_finalize",
            "mh_session_download", "mh_session_current_costs", "mh_session_summary", "mh_session_geometry",
-           "mh_session_destroy", "mh_debug_rng"]
+           "mh_session_destroy", "mh_debug_rng", "mh_debug_collectives"]
 
 P = C.POINTER
 
@@ -155,10 +155,12 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_session_current_costs.restype = C.c_int
     lib.mh_session_summary.argtypes = [C.c_void_p, P(mh_summary)]
     lib.mh_session_summary.restype = C.c_int
-    lib.mh_session_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int)]
+    lib.mh_session_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
     lib.mh_session_geometry.restype = C.c_int
     lib.mh_session_destroy.argtypes = [C.c_void_p]
     lib.mh_session_destroy.restype = None
+    lib.mh_debug_collectives.argtypes = [C.c_int, P(C.c_float), P(C.c_int), P(C.c_int)]
+    lib.mh_debug_collectives.restype = C.c_int
     lib.mh_debug_rng.argtypes = [C.c_uint64, C.c_uint64, C.c_int, P(C.c_uint32), P(C.c_float),
                                  P(C.c_float)]
     lib.mh_debug_rng.restype = C.c_int
@@ -269,6 +271,21 @@ def debug_rng(seed: int, subsequence: int, n: int):
             np.frombuffer(bytes(g), dtype=np.float32).copy())
 
 
+def debug_collectives(L: int, v, iv):
+    """The kernels' group collectives over groups of L lanes on 64 lane values (diagnostic)."""
+    lib = load_library()
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    iv = np.ascontiguousarray(iv, dtype=np.int32)
+    out = np.zeros(9 * 64, dtype=np.int32)
+    if lib.mh_debug_collectives(L, v.ctypes.data_as(P(C.c_float)), iv.ctypes.data_as(P(C.c_int)),
+                                out.ctypes.data_as(P(C.c_int))) != 0:
+        raise MHError(last_error(lib))
+    out = out.reshape(9, 64)
+    return {"m1": out[0].view(np.float32), "m2": out[1].view(np.float32), "j1": out[2],
+            "max": out[3].view(np.float32), "arg": out[4], "scan": out[5], "total": out[6],
+            "imax": out[7], "isum": out[8]}
+
+
 class Session:
     """Device-resident chains: the shard one rank owns (chain ids [offset, offset + chains))."""
 
@@ -315,9 +332,14 @@ class Session:
         return s
 
     def geometry(self):
-        lanes, cpw = C.c_int(), C.c_int()
-        self.lib.mh_session_geometry(self.h, C.byref(lanes), C.byref(cpw))
-        return lanes.value, cpw.value
+        """(lanes per chain, chains per workgroup) of the step kernel."""
+        return self.step_kernel()[:2]
+
+    def step_kernel(self):
+        """(lanes per chain, chains per workgroup, "incremental" | "full") of the step kernel."""
+        lanes, cpw, inc = C.c_int(), C.c_int(), C.c_int()
+        self.lib.mh_session_geometry(self.h, C.byref(lanes), C.byref(cpw), C.byref(inc))
+        return lanes.value, cpw.value, "incremental" if inc.value else "full"
 
     def close(self):
         if getattr(self, "h", None):

@@ -206,9 +206,45 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
 }
 
 struct Geometry {
-    int L, npl, waves;
+    int L, npl, waves;   // full-evaluation kernel (init, final, evaluation; step when !delta)
     mh::ChainLds lay;
+    bool delta;          // step with the incremental kernel (mh_delta.hip)
+    int dL, dwaves;
+    mh::DeltaLds dlay;
 };
+
+// Incremental step kernel geometry: 32 lanes per chain (measured best at N = 64..256) and the
+// waves per workgroup that keep the most chains resident per CU (LDS and the kernel's ~166
+// VGPRs = 12 waves per CU bound it). It is the default step from N = 100 up (config 5's N = 256:
+// 1.24e7 vs 9.4e6 chain-steps/s; at N <= 64 the full-evaluation kernel is faster).
+// $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES / $MH_DELTA_WAVES pin a shape.
+void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
+    g.dlay = mh::make_delta_layout(n, c, r);
+    const char* e = getenv("MH_DELTA");
+    g.delta = e && *e ? atoi(e) != 0 : n >= 100;
+    const int want_l = getenv("MH_DELTA_LANES") ? atoi(getenv("MH_DELTA_LANES")) : 32;
+    const int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
+    const int lds_cu = 160 * 1024, waves_cu_max = 12;
+    int best_chains = -1, best_waves = -1;
+    g.dL = 0;
+    for (int L : {8, 16, 32}) {
+        if (want_l && L != want_l) continue;
+        for (int w : {1, 2, 4}) {
+            if (want_w && w != want_w) continue;
+            const size_t b = mh::delta_lds_bytes(g.dlay, L, w);
+            if (b > (size_t)max_lds) continue;
+            const int waves = std::min((int)(lds_cu / b) * w, waves_cu_max / w * w);
+            const int chains = waves * (64 / L);
+            if (chains > best_chains || (chains == best_chains && waves > best_waves)) {
+                best_chains = chains;
+                best_waves = waves;
+                g.dL = L;
+                g.dwaves = w;
+            }
+        }
+    }
+    if (g.dL == 0) g.delta = false;  // does not fit: full evaluation
+}
 
 bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     g.L = mh::choose_lanes(n);
@@ -228,6 +264,7 @@ bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
         set_error("room does not fit in LDS");
         return false;
     }
+    choose_delta_geometry(n, c, r, max_lds, g);
     return true;
 }
 
@@ -272,6 +309,7 @@ struct mh_session {
         a.seed = seed;
         a.iterations = 0;
         a.lay = geo.lay;
+        a.dlay = geo.dlay;
         return a;
     }
 };
@@ -341,7 +379,8 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
     mh::LaunchArgs a = s->args();
     for (int done = 0; done < iterations; done += kStepsPerLaunch) {
         a.iterations = std::min(kStepsPerLaunch, iterations - done);
-        MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
+        if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dL, s->geo.dwaves, st));
+        else MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
     }
     return true;
 }
@@ -631,10 +670,14 @@ MH_API int mh_session_summary(mh_session* s, mh_summary* out) {
     return 0;
 }
 
-MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* chains_per_workgroup) {
+MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* chains_per_workgroup,
+                               int* incremental) {
     if (!s) { set_error("NULL session"); return -1; }
-    if (lanes_per_chain) *lanes_per_chain = s->geo.L;
-    if (chains_per_workgroup) *chains_per_workgroup = s->geo.waves * (64 / s->geo.L);
+    const int L = s->geo.delta ? s->geo.dL : s->geo.L;  // the step kernel's shape
+    const int w = s->geo.delta ? s->geo.dwaves : s->geo.waves;
+    if (lanes_per_chain) *lanes_per_chain = L;
+    if (chains_per_workgroup) *chains_per_workgroup = w * (64 / L);
+    if (incremental) *incremental = s->geo.delta ? 1 : 0;
     return 0;
 }
 
@@ -661,6 +704,31 @@ MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int
     (void)hipFree(d_n);
     if (e != hipSuccess) {
         set_error(std::string("mh_debug_rng: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+MH_API int mh_debug_collectives(int L, const float* v, const int* iv, int* out) {
+    if (!(L == 8 || L == 16 || L == 32 || L == 64) || !v || !iv || !out) {
+        set_error("bad arguments");
+        return -1;
+    }
+    float* d_v = nullptr;
+    int *d_iv = nullptr, *d_out = nullptr;
+    hipError_t e = hipMalloc((void**)&d_v, sizeof(float) * 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_iv, sizeof(int) * 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_out, sizeof(int) * 9 * 64);
+    if (e == hipSuccess) e = hipMemcpy(d_v, v, sizeof(float) * 64, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_iv, iv, sizeof(int) * 64, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mh::launch_collectives(L, d_v, d_iv, d_out, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(int) * 9 * 64, hipMemcpyDeviceToHost);
+    (void)hipFree(d_v);
+    (void)hipFree(d_iv);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) {
+        set_error(std::string("mh_debug_collectives: ") + hipGetErrorString(e));
         return -1;
     }
     return 0;

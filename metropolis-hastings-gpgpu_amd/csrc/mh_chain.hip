@@ -17,20 +17,13 @@
 //     draw count, so k launches of m steps equal one launch of k*m steps.
 // Compiled with -ffp-contract=off: every multiply and add rounds where the reference's does.
 
-#include <hip/hip_runtime.h>
-#include <rocrand/rocrand_philox4x32_10.h>
-#include <rocrand/rocrand_uniform.h>
-
 #include <stdint.h>
 #include <stdlib.h>
 
-#include "mh_launch.h"
-
-#ifndef MH_ABLATE
-#define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
-#endif
+#include "mh_common.h"
 #ifndef MH_DOUBLE
 #define MH_DOUBLE 0  // cost-probe builds: run phase k twice when bit k is set; product = 0
+                     // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay)
 #endif
 #define MH_REPS(bit) ((MH_DOUBLE & (bit)) ? 2 : 1)
 #define MH_CLOBBER() asm volatile("" ::: "memory")
@@ -48,12 +41,6 @@ __device__ unsigned long long g_phase_cycles[16];
 #endif
 
 namespace mh {
-
-struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
-    float xf, yf;  // (float)x, (float)y -- every O(N^2) use of x, y is through float args
-    float rotYf;   // (float)rotY
-    float pad;
-};
 
 struct Backup {  // the cost-relevant pose of one object (z, rotX, rotZ never enter a cost)
     int k;
@@ -91,284 +78,6 @@ struct ChainPtrs {
     ChainAux* aux;
 };
 
-// ---- wave-level helpers -----------------------------------------------------------------
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int L>
-__device__ __forceinline__ uint64_t group_ballot(bool pred, int gbase) {
-    uint64_t b = __ballot(pred);
-    if constexpr (L == 64) {
-        return b;
-    } else {
-        return (b >> gbase) & ((1ull << L) - 1ull);
-    }
-}
-
-// Value of v held by lane `src` of this lane's group (src is group-uniform).
-template <int L>
-__device__ __forceinline__ float grp_get(float v, int src, int gbase) {
-    if constexpr (L == 64) {
-        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
-    } else {
-        return __int_as_float(__builtin_amdgcn_ds_bpermute((gbase + src) << 2, __float_as_int(v)));
-    }
-}
-
-template <int L>
-__device__ __forceinline__ double grp_get(double v, int src, int gbase) {
-    int2 w = *reinterpret_cast<int2*>(&v);
-    int2 o;
-    if constexpr (L == 64) {
-        o.x = __builtin_amdgcn_readlane(w.x, src);
-        o.y = __builtin_amdgcn_readlane(w.y, src);
-    } else {
-        o.x = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.x);
-        o.y = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.y);
-    }
-    return *reinterpret_cast<double*>(&o);
-}
-
-// ---- RNG ----------------------------------------------------------------------------------
-
-// Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
-// OCML log/sin/cos code is not duplicated at every call site.
-__device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
-    if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
-    const double u1 = (double)a * 0x1p-32 + 0x1p-33;
-    const double u2 = (double)b * 0x1p-32 + 0x1p-33;
-    const double rad = sqrt(-2.0 * log(u1));
-    const double ang = 6.283185307179586 * u2;
-    return make_float2((float)(rad * sin(ang)), (float)(rad * cos(ang)));
-}
-
-// rocRAND Philox4x32-10 stream of one chain. Words are taken a block of four at a time with
-// rocrand4() (identical to four rocrand() calls from substate 0) and selected without dynamic
-// register indexing, so the state stays in registers.
-struct ChainRng {
-    rocrand_state_philox4x32_10 st;
-    uint4 buf;          // current block
-    int idx;            // next word of buf (4 = exhausted)
-    uint64_t draws;     // words consumed since draw 0
-    int bm_has;
-    float bm_val;
-
-    __device__ __forceinline__ void init(uint64_t seed, uint64_t subsequence, uint64_t offset) {
-        rocrand_init(seed, subsequence, offset & ~3ull, &st);
-        buf = rocrand4(&st);
-        idx = (int)(offset & 3);
-        draws = offset;
-    }
-    __device__ __forceinline__ unsigned int next() {
-        if (idx == 4) {
-            buf = rocrand4(&st);
-            idx = 0;
-        }
-        const unsigned int v = idx == 0 ? buf.x : idx == 1 ? buf.y : idx == 2 ? buf.z : buf.w;
-        ++idx;
-        ++draws;
-        return v;
-    }
-    // curand_uniform stand-in (Kernel.cu:569,710): rocRAND's (0,1] float conversion.
-    __device__ __forceinline__ float uniform() {
-        return rocrand_device::detail::uniform_distribution(next());
-    }
-    // curand_normal stand-in (Kernel.cu:605,608,641): sine branch first, cosine branch cached
-    // for the next call (cuRAND's caching order).
-    __device__ __forceinline__ float normal() {
-        if (bm_has) {
-            bm_has = 0;
-            return bm_val;
-        }
-        const unsigned int a = next();
-        const unsigned int b = next();
-        const float2 z = box_muller(a, b);
-        bm_val = z.y;
-        bm_has = 1;
-        return z.x;
-    }
-};
-
-// ---- numerics shared by every term ---------------------------------------------------------
-
-// Kernel.cu:162-167: float difference, double root.
-__device__ __forceinline__ double distance_f(float xi, float yi, float xj, float yj) {
-    float fx = xi - xj;
-    float fy = yi - yj;
-    double dx = fx, dy = fy;
-    double sq = dx * dx;
-    sq = sq + dy * dy;
-    return sqrt(sq);
-}
-
-// Kernel.cu:170-182.
-__device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {
-    double dx = (double)(float)(xi - xj);
-    double dy = (double)(float)(yi - yj);
-    double tp = atan2(dy, dx);
-    if (tp < 0) tp = kTwoPI + tp;
-    double t = tp - (double)ti;
-    return (t < 0) ? kTwoPI + t : t;
-}
-
-// The reference's float atan2f / cosf, evaluated as the double function rounded once.
-__device__ __forceinline__ float atan2_f32(float y, float x) {
-    return (float)atan2((double)y, (double)x);
-}
-__device__ __forceinline__ float cos_f32(float x) { return (float)cos((double)x); }
-
-// minValue/maxValue (Kernel.cu:366-401) of a rectangle translated by (tx, ty), as floats.
-__device__ __forceinline__ float4 shape_box(const RectShape& s, float tx, float ty) {
-    float4 b;
-    b.x = fminf(s.v0x, (float)(s.xmin1 + (double)tx));
-    b.y = (float)(s.ymin + (double)ty);
-    b.z = (float)(s.xmax + (double)tx);
-    b.w = (float)(s.ymax + (double)ty);
-    return b;
-}
-
-// calculateIntersectionArea, Kernel.cu:321-340 (boxes already rounded to float).
-__device__ __forceinline__ float overlap(float4 a, float4 b) {
-    float x5 = fmaxf(a.x, b.x);
-    float y5 = fmaxf(a.y, b.y);
-    float x6 = fminf(a.z, b.z);
-    float y6 = fminf(a.w, b.w);
-    if (x5 >= x6 || y5 >= y6) return 0.0f;
-    return (x6 - x5) * (y6 - y5);
-}
-
-__device__ __forceinline__ float4 comp_overlaps(const DevRoom& rm, float4 box) {
-    float4 t;
-    t.x = overlap(box, make_float4(rm.comp[0][0], rm.comp[0][1], rm.comp[0][2], rm.comp[0][3]));
-    t.y = overlap(box, make_float4(rm.comp[1][0], rm.comp[1][1], rm.comp[1][2], rm.comp[1][3]));
-    t.z = overlap(box, make_float4(rm.comp[2][0], rm.comp[2][1], rm.comp[2][2], rm.comp[2][3]));
-    t.w = overlap(box, make_float4(rm.comp[3][0], rm.comp[3][1], rm.comp[3][2], rm.comp[3][3]));
-    return t;
-}
-
-__device__ __forceinline__ bool nonzero4(float4 t) {
-    return t.x != 0.0f || t.y != 0.0f || t.z != 0.0f || t.w != 0.0f;
-}
-
-// Serially subtract, in lane order, the float4 terms of the group's lanes that are non-zero.
-template <int L>
-__device__ __forceinline__ float serial_sub4(float acc, float4 t, int gbase) {
-    uint64_t bits = group_ballot<L>(nonzero4(t), gbase);
-    while (bits) {
-        int b = __builtin_ctzll(bits);
-        bits &= bits - 1;
-        acc = acc - grp_get<L>(t.x, b, gbase);
-        acc = acc - grp_get<L>(t.y, b, gbase);
-        acc = acc - grp_get<L>(t.z, b, gbase);
-        acc = acc - grp_get<L>(t.w, b, gbase);
-    }
-    return acc;
-}
-
-template <int L>
-__device__ __forceinline__ float serial_sub(float acc, float t, int gbase) {
-    uint64_t bits = group_ballot<L>(t != 0.0f, gbase);
-    while (bits) {
-        int b = __builtin_ctzll(bits);
-        bits &= bits - 1;
-        acc = acc - grp_get<L>(t, b, gbase);
-    }
-    return acc;
-}
-
-template <int L>
-__device__ __forceinline__ double serial_sub(double acc, double t, int gbase) {
-    uint64_t bits = group_ballot<L>(t != 0.0, gbase);
-    while (bits) {
-        int b = __builtin_ctzll(bits);
-        bits &= bits - 1;
-        acc = acc - grp_get<L>(t, b, gbase);
-    }
-    return acc;
-}
-
-// One symmetry pair exactly as Kernel.cu:305-310 computes it, for the reflected row pose
-// (rx, ry, rr) and object j's pose (xj, yj, ryj).
-__device__ __forceinline__ float sym_val_exact(float xj, float yj, double ryj, float rx, float ry,
-                                               double rr) {
-    const float dp = (float)distance_f(xj, yj, rx, ry);
-    float dt = (float)(ryj - rr);
-    if (dt > kPI) dt = (float)((double)dt - kTwoPI);
-    const float head = 5.0f - sqrtf(dp);
-    return (float)((double)head - 0.4 * (double)fabsf(dt));
-}
-
-// fp32 estimate of sym_val_exact from q = {xf, yf, rotYf, -}: exact float differences,
-// hardware (1 ulp) square roots, fp32 wrap and combine.
-__device__ __forceinline__ float sym_val_fast(float4 q, float rx, float ry, float rr) {
-    const float dx = q.x - rx;
-    const float dy = q.y - ry;
-    const float s = fmaf(dx, dx, dy * dy);
-    const float h = __builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf(s));
-    float dt = q.z - rr;
-    dt = (dt > 3.1416f) ? dt - 6.2832f : dt;
-    return fmaf(-0.4f, fabsf(dt), 5.0f - h);
-}
-
-// Bound on |sym_val_fast - sym_val_exact| for an estimate v in a row with reflected angle rr,
-// for poses with |x|, |y|, |rotY| < 1e15. Derivation (DESIGN.md "Symmetry estimate"): the
-// square-root chain contributes <= 2^-21 (5 + |v|), the rotation difference and wrap <= 2^-22
-// (12.6 + 2|v| + |rr|) x 0.4, the fp32 combine <= 2^-23 (15 + 2|v|) and the reference's own
-// final rounding 2^-24 |v|; together < 2^-21 (12 + 2.2|v| + 0.1|rr|). A 4x margin gives:
-__device__ __forceinline__ float sym_err(float v, float rr) {
-    return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
-}
-
-// Group-wide top two of (m1, m2) with the argmax of m1, butterfly over the group's lanes.
-template <int L>
-__device__ __forceinline__ void group_top2(float& m1, float& m2, int& j1) {
-#pragma unroll
-    for (int off = L / 2; off > 0; off >>= 1) {
-        const float p1 = __shfl_xor(m1, off);
-        const float p2 = __shfl_xor(m2, off);
-        const int pj = __shfl_xor(j1, off);
-        const float lo = fminf(m1, p1);
-        const bool take = p1 > m1 || (p1 == m1 && pj < j1);  // ties: lowest index on every lane
-        m2 = fmaxf(lo, fmaxf(m2, p2));
-        m1 = fmaxf(m1, p1);
-        j1 = take ? pj : j1;
-    }
-}
-
-// Group-wide maximum of v with its index (ties: lowest index).
-template <int L>
-__device__ __forceinline__ void group_max_arg(float& v, int& j) {
-#pragma unroll
-    for (int off = L / 2; off > 0; off >>= 1) {
-        const float pv = __shfl_xor(v, off);
-        const int pj = __shfl_xor(j, off);
-        const bool take = pv > v || (pv == v && pj < j);
-        v = take ? pv : v;
-        j = take ? pj : j;
-    }
-}
-
-// a[m] for a runtime m, as a select chain (no dynamic register indexing).
-template <int NPL, typename T>
-__device__ __forceinline__ T sel(const T (&a)[NPL], int m) {
-    T v = a[0];
-#pragma unroll
-    for (int q = 1; q < NPL; ++q) v = (m == q) ? a[q] : v;
-    return v;
-}
-
-// Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that
-// attains each (-1: the 0 floor of Kernel.cu:303 is the maximum).
-template <int NPL>
-struct SymRows {
-    float mx[NPL];
-    int arg[NPL];
-};
-
 // ---- compacted term lists for the ordered sums -------------------------------------------
 //
 // Clearance terms (floats, capacity 2L) and PairWise / Angle terms (doubles, capacity lst_r =
@@ -400,30 +109,9 @@ __device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& a
     cnt += __builtin_popcountll(b);
 }
 
-// PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
+// PairWiseCosts / PairWiseAngleCosts terms of relationship q (mh_common.h).
 __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tpw, double& tang) {
-    tpw = 0.0;
-    tang = 0.0;
-    const RelConst rc = ch.relc[q];
-    const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
-    const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
-    if (d < rc.start) {
-        double f = d / rc.start;
-        tpw = f * f;
-    } else if (d > rc.end) {
-        double f = rc.end / d;
-        tpw = f * f;
-    }
-    const ObjP as = ch.P[rc.as], at = ch.P[rc.at];
-    const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
-    if (rc.amin > rc.amax) {
-        double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
-        float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
-        if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
-    } else if (rc.amin < th || th < rc.amax) {
-        double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
-        tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
-    }
+    rel_terms(ch.relc[q], ch.P, tpw, tang);
 }
 
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
@@ -586,6 +274,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // unless a changed column beats it (screened by the estimate) or its argmax column is a
     // changed one whose value dropped; changed rows and such rows are re-scanned by the whole
     // group, one row at a time.
+    for (int rep = 0; rep < MH_REPS(64); ++rep) {
+    MH_CLOBBER();
     bool need[NPL];
     unsigned pend[NPL];
     float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
@@ -714,6 +404,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             }
             any_row |= rows[m] != 0;
         }
+    }
     }
     }
 
@@ -895,19 +586,6 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
 
 // ---- propose(), Kernel.cu:566-704, applied in place --------------------------------------
 
-__device__ __forceinline__ int rand_int(ChainRng& rng, int max, int min) {
-    float u = rng.uniform();
-    u = (float)((double)u * ((double)(max - min) + 0.999999));
-    u = u + (float)min;
-    return (int)truncf(u);
-}
-
-__device__ __forceinline__ int pick_object(ChainRng& rng, int n, const unsigned char* frozen) {
-    int k = rand_int(rng, n - 1, 0);
-    while (frozen[k]) k = rand_int(rng, n - 1, 0);  // frozen[n] == 1: index n is redrawn
-    return k;
-}
-
 __device__ __forceinline__ Backup read_obj(const ChainPtrs& ch, int k) {
     Backup b;
     b.k = k;
@@ -1019,13 +697,6 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
         const Backup b = ch.aux->b[q];
         write_obj(ch, b.k, b.x, b.y, b.ry);
     }
-}
-
-// Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
-__device__ __forceinline__ bool accept(ChainRng& rng, float star, float cur) {
-    const float u = rng.uniform();
-    const float thr = fminf(1.0f, (float)exp(kBeta * ((double)star - (double)cur)));
-    return u < thr;
 }
 
 // ---- the kernel ---------------------------------------------------------------------------
@@ -1277,6 +948,34 @@ __global__ void mh_rng_kernel(uint64_t seed, uint64_t subsequence, int n, unsign
     for (int i = 0; i < n; ++i) nrm[i] = r.normal();
 }
 
+// ---- diagnostic: the group collectives on given lane values ---------------------------------
+
+// out[k * 64 + lane] for k = 0 top-2 m1, 1 m2, 2 argmax (lane index within the group, values
+// v), 3 max-with-index value, 4 its index, 5 exclusive scan of iv, 6 its group total,
+// 7 group max of iv, 8 group sum of iv (floats as bits).
+template <int L>
+__global__ void mh_collectives_kernel(const float* v, const int* iv, int* out) {
+    const int lane = threadIdx.x;
+    const int r = lane % L;
+    float m1 = v[lane], m2 = -INFINITY;
+    int j1 = r;
+    group_top2<L>(m1, m2, j1);
+    float mv = v[lane];
+    int mj = r;
+    group_max_arg<L>(mv, mj);
+    int tot;
+    const int ex = group_excl_scan<L>(iv[lane], r, tot);
+    out[0 * 64 + lane] = __float_as_int(m1);
+    out[1 * 64 + lane] = __float_as_int(m2);
+    out[2 * 64 + lane] = j1;
+    out[3 * 64 + lane] = __float_as_int(mv);
+    out[4 * 64 + lane] = mj;
+    out[5 * 64 + lane] = ex;
+    out[6 * 64 + lane] = tot;
+    out[7 * 64 + lane] = group_max<L>(iv[lane]);
+    out[8 * 64 + lane] = group_sum<L>(iv[lane]);
+}
+
 // ---- host-side launch dispatch ------------------------------------------------------------
 
 template <int L, int NPL>
@@ -1359,6 +1058,16 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsi
                    hipSuccess ? 0 : -1;
 }
 #endif
+
+hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hipStream_t s) {
+    switch (L) {
+        case 8: hipLaunchKernelGGL(mh_collectives_kernel<8>, dim3(1), dim3(64), 0, s, v, iv, out); break;
+        case 16: hipLaunchKernelGGL(mh_collectives_kernel<16>, dim3(1), dim3(64), 0, s, v, iv, out); break;
+        case 32: hipLaunchKernelGGL(mh_collectives_kernel<32>, dim3(1), dim3(64), 0, s, v, iv, out); break;
+        default: hipLaunchKernelGGL(mh_collectives_kernel<64>, dim3(1), dim3(64), 0, s, v, iv, out); break;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
                       float* nrm, hipStream_t s) {

@@ -1,0 +1,448 @@
+// mh_common.h -- device code shared by the step kernels (mh_chain.hip: full evaluation,
+// mh_delta.hip: incremental evaluation): the RNG, the reference's numerics for every cost term,
+// the proposal draws and the accept rule. Everything here rounds exactly where
+// KernelFolder/Kernel/Kernel.cu does (compile with -ffp-contract=off).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rocrand/rocrand_philox4x32_10.h>
+#include <rocrand/rocrand_uniform.h>
+
+#include <stdint.h>
+
+#include "mh_launch.h"
+
+#ifndef MH_ABLATE
+#define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
+#endif
+
+namespace mh {
+
+struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
+    float xf, yf;  // (float)x, (float)y -- every O(N^2) use of x, y is through float args
+    float rotYf;   // (float)rotY
+    float pad;
+};
+
+// ---- wave-level helpers -----------------------------------------------------------------
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int L>
+__device__ __forceinline__ uint64_t group_ballot(bool pred, int gbase) {
+    uint64_t b = __ballot(pred);
+    if constexpr (L == 64) {
+        return b;
+    } else {
+        return (b >> gbase) & ((1ull << L) - 1ull);
+    }
+}
+
+// Value of v held by lane `src` of this lane's group (src is group-uniform).
+template <int L>
+__device__ __forceinline__ float grp_get(float v, int src, int gbase) {
+    if constexpr (L == 64) {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+    } else {
+        return __int_as_float(__builtin_amdgcn_ds_bpermute((gbase + src) << 2, __float_as_int(v)));
+    }
+}
+
+template <int L>
+__device__ __forceinline__ double grp_get(double v, int src, int gbase) {
+    int2 w = *reinterpret_cast<int2*>(&v);
+    int2 o;
+    if constexpr (L == 64) {
+        o.x = __builtin_amdgcn_readlane(w.x, src);
+        o.y = __builtin_amdgcn_readlane(w.y, src);
+    } else {
+        o.x = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.x);
+        o.y = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.y);
+    }
+    return *reinterpret_cast<double*>(&o);
+}
+
+// ---- RNG ----------------------------------------------------------------------------------
+
+// Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
+// OCML log/sin/cos code is not duplicated at every call site.
+static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
+    if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
+    const double u1 = (double)a * 0x1p-32 + 0x1p-33;
+    const double u2 = (double)b * 0x1p-32 + 0x1p-33;
+    const double rad = sqrt(-2.0 * log(u1));
+    const double ang = 6.283185307179586 * u2;
+    return make_float2((float)(rad * sin(ang)), (float)(rad * cos(ang)));
+}
+
+// rocRAND Philox4x32-10 stream of one chain. Words are taken a block of four at a time with
+// rocrand4() (identical to four rocrand() calls from substate 0) and selected without dynamic
+// register indexing, so the state stays in registers.
+struct ChainRng {
+    rocrand_state_philox4x32_10 st;
+    uint4 buf;          // current block
+    int idx;            // next word of buf (4 = exhausted)
+    uint64_t draws;     // words consumed since draw 0
+    int bm_has;
+    float bm_val;
+
+    __device__ __forceinline__ void init(uint64_t seed, uint64_t subsequence, uint64_t offset) {
+        rocrand_init(seed, subsequence, offset & ~3ull, &st);
+        buf = rocrand4(&st);
+        idx = (int)(offset & 3);
+        draws = offset;
+    }
+    __device__ __forceinline__ unsigned int next() {
+        if (idx == 4) {
+            buf = rocrand4(&st);
+            idx = 0;
+        }
+        const unsigned int v = idx == 0 ? buf.x : idx == 1 ? buf.y : idx == 2 ? buf.z : buf.w;
+        ++idx;
+        ++draws;
+        return v;
+    }
+    // curand_uniform stand-in (Kernel.cu:569,710): rocRAND's (0,1] float conversion.
+    __device__ __forceinline__ float uniform() {
+        return rocrand_device::detail::uniform_distribution(next());
+    }
+    // curand_normal stand-in (Kernel.cu:605,608,641): sine branch first, cosine branch cached
+    // for the next call (cuRAND's caching order).
+    __device__ __forceinline__ float normal() {
+        if (bm_has) {
+            bm_has = 0;
+            return bm_val;
+        }
+        const unsigned int a = next();
+        const unsigned int b = next();
+        const float2 z = box_muller(a, b);
+        bm_val = z.y;
+        bm_has = 1;
+        return z.x;
+    }
+};
+
+// ---- numerics shared by every term ---------------------------------------------------------
+
+// Kernel.cu:162-167: float difference, double root.
+__device__ __forceinline__ double distance_f(float xi, float yi, float xj, float yj) {
+    float fx = xi - xj;
+    float fy = yi - yj;
+    double dx = fx, dy = fy;
+    double sq = dx * dx;
+    sq = sq + dy * dy;
+    return sqrt(sq);
+}
+
+// Kernel.cu:170-182.
+__device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {
+    double dx = (double)(float)(xi - xj);
+    double dy = (double)(float)(yi - yj);
+    double tp = atan2(dy, dx);
+    if (tp < 0) tp = kTwoPI + tp;
+    double t = tp - (double)ti;
+    return (t < 0) ? kTwoPI + t : t;
+}
+
+// The reference's float atan2f / cosf, evaluated as the double function rounded once.
+__device__ __forceinline__ float atan2_f32(float y, float x) {
+    return (float)atan2((double)y, (double)x);
+}
+__device__ __forceinline__ float cos_f32(float x) { return (float)cos((double)x); }
+
+// minValue/maxValue (Kernel.cu:366-401) of a rectangle translated by (tx, ty), as floats.
+__device__ __forceinline__ float4 shape_box(const RectShape& s, float tx, float ty) {
+    float4 b;
+    b.x = fminf(s.v0x, (float)(s.xmin1 + (double)tx));
+    b.y = (float)(s.ymin + (double)ty);
+    b.z = (float)(s.xmax + (double)tx);
+    b.w = (float)(s.ymax + (double)ty);
+    return b;
+}
+
+// calculateIntersectionArea, Kernel.cu:321-340 (boxes already rounded to float).
+__device__ __forceinline__ float overlap(float4 a, float4 b) {
+    float x5 = fmaxf(a.x, b.x);
+    float y5 = fmaxf(a.y, b.y);
+    float x6 = fminf(a.z, b.z);
+    float y6 = fminf(a.w, b.w);
+    if (x5 >= x6 || y5 >= y6) return 0.0f;
+    return (x6 - x5) * (y6 - y5);
+}
+
+__device__ __forceinline__ float4 comp_overlaps(const DevRoom& rm, float4 box) {
+    float4 t;
+    t.x = overlap(box, make_float4(rm.comp[0][0], rm.comp[0][1], rm.comp[0][2], rm.comp[0][3]));
+    t.y = overlap(box, make_float4(rm.comp[1][0], rm.comp[1][1], rm.comp[1][2], rm.comp[1][3]));
+    t.z = overlap(box, make_float4(rm.comp[2][0], rm.comp[2][1], rm.comp[2][2], rm.comp[2][3]));
+    t.w = overlap(box, make_float4(rm.comp[3][0], rm.comp[3][1], rm.comp[3][2], rm.comp[3][3]));
+    return t;
+}
+
+__device__ __forceinline__ bool nonzero4(float4 t) {
+    return t.x != 0.0f || t.y != 0.0f || t.z != 0.0f || t.w != 0.0f;
+}
+
+// Serially subtract, in lane order, the float4 terms of the group's lanes that are non-zero.
+template <int L>
+__device__ __forceinline__ float serial_sub4(float acc, float4 t, int gbase) {
+    uint64_t bits = group_ballot<L>(nonzero4(t), gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t.x, b, gbase);
+        acc = acc - grp_get<L>(t.y, b, gbase);
+        acc = acc - grp_get<L>(t.z, b, gbase);
+        acc = acc - grp_get<L>(t.w, b, gbase);
+    }
+    return acc;
+}
+
+template <int L>
+__device__ __forceinline__ float serial_sub(float acc, float t, int gbase) {
+    uint64_t bits = group_ballot<L>(t != 0.0f, gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t, b, gbase);
+    }
+    return acc;
+}
+
+template <int L>
+__device__ __forceinline__ double serial_sub(double acc, double t, int gbase) {
+    uint64_t bits = group_ballot<L>(t != 0.0, gbase);
+    while (bits) {
+        int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        acc = acc - grp_get<L>(t, b, gbase);
+    }
+    return acc;
+}
+
+// One symmetry pair exactly as Kernel.cu:305-310 computes it, for the reflected row pose
+// (rx, ry, rr) and object j's pose (xj, yj, ryj).
+__device__ __forceinline__ float sym_val_exact(float xj, float yj, double ryj, float rx, float ry,
+                                               double rr) {
+    const float dp = (float)distance_f(xj, yj, rx, ry);
+    float dt = (float)(ryj - rr);
+    if (dt > kPI) dt = (float)((double)dt - kTwoPI);
+    const float head = 5.0f - sqrtf(dp);
+    return (float)((double)head - 0.4 * (double)fabsf(dt));
+}
+
+// fp32 estimate of sym_val_exact from q = {xf, yf, rotYf, -}: exact float differences,
+// hardware (1 ulp) square roots, fp32 wrap and combine.
+__device__ __forceinline__ float sym_val_fast(float4 q, float rx, float ry, float rr) {
+    const float dx = q.x - rx;
+    const float dy = q.y - ry;
+    const float s = fmaf(dx, dx, dy * dy);
+    const float h = __builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf(s));
+    float dt = q.z - rr;
+    dt = (dt > 3.1416f) ? dt - 6.2832f : dt;
+    return fmaf(-0.4f, fabsf(dt), 5.0f - h);
+}
+
+// Bound on |sym_val_fast - sym_val_exact| for an estimate v in a row with reflected angle rr,
+// for poses with |x|, |y|, |rotY| < 1e15. Derivation (DESIGN.md "Symmetry estimate"): the
+// square-root chain contributes <= 2^-21 (5 + |v|), the rotation difference and wrap <= 2^-22
+// (12.6 + 2|v| + |rr|) x 0.4, the fp32 combine <= 2^-23 (15 + 2|v|) and the reference's own
+// final rounding 2^-24 |v|; together < 2^-21 (12 + 2.2|v| + 0.1|rr|). A 4x margin gives:
+__device__ __forceinline__ float sym_err(float v, float rr) {
+    return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
+}
+
+// ---- group collectives over the L lanes of one chain, in registers (DPP / permlane) ---------
+//
+// Butterfly partner at level OFF: lane ^ 1 and lane ^ 2 (DPP quad_perm), the mirrored quad /
+// half-row for 4 and 8 (DPP row_half_mirror / row_mirror -- the same partner block as lane ^ OFF,
+// which is all a reduction needs once values are uniform within each OFF-block), lane ^ 16 and
+// lane ^ 32 (gfx950 v_permlane16_swap / v_permlane32_swap). None of them goes through LDS.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND_ZERO = false>
+__device__ __forceinline__ int dpp_mov(int v, int old = 0) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO);
+}
+
+template <int OFF>
+__device__ __forceinline__ int bfly(int v) {
+    if constexpr (OFF == 1) {
+        return dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    } else if constexpr (OFF == 2) {
+        return dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    } else if constexpr (OFF == 4) {
+        return dpp_mov<0x141>(v);  // row_half_mirror
+    } else if constexpr (OFF == 8) {
+        return dpp_mov<0x140>(v);  // row_mirror
+    } else if constexpr (OFF == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return ((__lane_id() >> 4) & 1) ? (int)p[0] : (int)p[1];
+    } else {
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (__lane_id() >> 5) ? (int)p[0] : (int)p[1];
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ float bfly(float v) {
+    return __int_as_float(bfly<OFF>(__float_as_int(v)));
+}
+
+// Group-wide top two of (m1, m2) with the argmax of m1 (ties: lowest index, on every lane).
+template <int L>
+__device__ __forceinline__ void group_top2(float& m1, float& m2, int& j1) {
+    auto level = [&](float p1, float p2, int pj) {
+        const float lo = fminf(m1, p1);
+        const bool take = p1 > m1 || (p1 == m1 && pj < j1);
+        m2 = fmaxf(lo, fmaxf(m2, p2));
+        m1 = fmaxf(m1, p1);
+        j1 = take ? pj : j1;
+    };
+    level(bfly<1>(m1), bfly<1>(m2), bfly<1>(j1));
+    level(bfly<2>(m1), bfly<2>(m2), bfly<2>(j1));
+    if constexpr (L >= 8) level(bfly<4>(m1), bfly<4>(m2), bfly<4>(j1));
+    if constexpr (L >= 16) level(bfly<8>(m1), bfly<8>(m2), bfly<8>(j1));
+    if constexpr (L >= 32) level(bfly<16>(m1), bfly<16>(m2), bfly<16>(j1));
+    if constexpr (L >= 64) level(bfly<32>(m1), bfly<32>(m2), bfly<32>(j1));
+}
+
+// Group-wide maximum of v with its index (ties: lowest index).
+template <int L>
+__device__ __forceinline__ void group_max_arg(float& v, int& j) {
+    auto level = [&](float pv, int pj) {
+        const bool take = pv > v || (pv == v && pj < j);
+        v = take ? pv : v;
+        j = take ? pj : j;
+    };
+    level(bfly<1>(v), bfly<1>(j));
+    level(bfly<2>(v), bfly<2>(j));
+    if constexpr (L >= 8) level(bfly<4>(v), bfly<4>(j));
+    if constexpr (L >= 16) level(bfly<8>(v), bfly<8>(j));
+    if constexpr (L >= 32) level(bfly<16>(v), bfly<16>(j));
+    if constexpr (L >= 64) level(bfly<32>(v), bfly<32>(j));
+}
+
+// Group-wide integer max / sum.
+template <int L>
+__device__ __forceinline__ int group_max(int v) {
+    v = max(v, bfly<1>(v));
+    v = max(v, bfly<2>(v));
+    if constexpr (L >= 8) v = max(v, bfly<4>(v));
+    if constexpr (L >= 16) v = max(v, bfly<8>(v));
+    if constexpr (L >= 32) v = max(v, bfly<16>(v));
+    if constexpr (L >= 64) v = max(v, bfly<32>(v));
+    return v;
+}
+
+template <int L>
+__device__ __forceinline__ int group_sum(int v) {
+    v += bfly<1>(v);
+    v += bfly<2>(v);
+    if constexpr (L >= 8) v += bfly<4>(v);
+    if constexpr (L >= 16) v += bfly<8>(v);
+    if constexpr (L >= 32) v += bfly<16>(v);
+    if constexpr (L >= 64) v += bfly<32>(v);
+    return v;
+}
+
+// Exclusive prefix sum over the group's lanes (r = lane within the group) and the group total.
+// Inclusive scan by DPP row_shr within 16-lane rows (zero-filled at the row start, masked at an
+// 8-lane group start), then row_bcast15 / row_bcast31 across rows.
+template <int L>
+__device__ __forceinline__ int group_excl_scan(int v, int r, int& total) {
+    int x = v;
+    int t = dpp_mov<0x111, 0xF, 0xF, true>(x);  // row_shr:1
+    x += (r >= 1) ? t : 0;
+    t = dpp_mov<0x112, 0xF, 0xF, true>(x);      // row_shr:2
+    x += (r >= 2) ? t : 0;
+    t = dpp_mov<0x114, 0xF, 0xF, true>(x);      // row_shr:4
+    x += (r >= 4) ? t : 0;
+    if constexpr (L >= 16) {
+        t = dpp_mov<0x118, 0xF, 0xF, true>(x);  // row_shr:8
+        x += t;
+    }
+    if constexpr (L >= 32) {
+        t = dpp_mov<0x142, 0xA, 0xF, false>(x, 0);  // row_bcast15 into rows 1 and 3
+        x += t;
+    }
+    if constexpr (L >= 64) {
+        t = dpp_mov<0x143, 0xC, 0xF, false>(x, 0);  // row_bcast31 into rows 2 and 3
+        x += t;
+    }
+    if constexpr (L == 64) {
+        total = __builtin_amdgcn_readlane(x, 63);
+    } else {
+        total = __shfl(x, (__lane_id() & ~(L - 1)) + L - 1);
+    }
+    return x - v;
+}
+
+// a[m] for a runtime m, as a select chain (no dynamic register indexing).
+template <int NPL, typename T>
+__device__ __forceinline__ T sel(const T (&a)[NPL], int m) {
+    T v = a[0];
+#pragma unroll
+    for (int q = 1; q < NPL; ++q) v = (m == q) ? a[q] : v;
+    return v;
+}
+
+// Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that
+// attains each (-1: the 0 floor of Kernel.cu:303 is the maximum).
+template <int NPL>
+struct SymRows {
+    float mx[NPL];
+    int arg[NPL];
+};
+
+// PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
+__device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, double& tpw,
+                                          double& tang) {
+    tpw = 0.0;
+    tang = 0.0;
+    const ObjP ps = P[rc.s], pt = P[rc.t];
+    const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
+    if (d < rc.start) {
+        double f = d / rc.start;
+        tpw = f * f;
+    } else if (d > rc.end) {
+        double f = rc.end / d;
+        tpw = f * f;
+    }
+    const ObjP as = P[rc.as], at = P[rc.at];
+    const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
+    if (rc.amin > rc.amax) {
+        double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
+        float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
+        if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+    } else if (rc.amin < th || th < rc.amax) {
+        double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
+        tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+    }
+}
+
+// ---- proposal draws and the accept rule ----------------------------------------------------
+
+__device__ __forceinline__ int rand_int(ChainRng& rng, int max, int min) {
+    float u = rng.uniform();
+    u = (float)((double)u * ((double)(max - min) + 0.999999));
+    u = u + (float)min;
+    return (int)truncf(u);
+}
+
+__device__ __forceinline__ int pick_object(ChainRng& rng, int n, const unsigned char* frozen) {
+    int k = rand_int(rng, n - 1, 0);
+    while (frozen[k]) k = rand_int(rng, n - 1, 0);  // frozen[n] == 1: index n is redrawn
+    return k;
+}
+
+// Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
+__device__ __forceinline__ bool accept(ChainRng& rng, float star, float cur) {
+    const float u = rng.uniform();
+    const float thr = fminf(1.0f, (float)exp(kBeta * ((double)star - (double)cur)));
+    return u < thr;
+}
+
+}  // namespace mh

@@ -109,15 +109,84 @@ struct ChainLds {
 
 inline MH_HD int round16(int v) { return (v + 15) & ~15; }
 
+// LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables as in
+// ChainLds plus three replay streams (areas, ones, zeros), then per chain the configuration and
+// every cached quantity a proposal changes only locally. The replay reads each ordered sum as a
+// stream of NP = round4(N + 1) entries, zero past its end (sentinels / zero fill).
+struct DeltaLds {
+    int hdr, h_obj, h_clr, h_rel, h_frz, h_room;
+    int h_area, h_ones, h_zero;  // float[NP] areas, float[NP] ones, double[NP] zeros
+    int NP;
+    int X, Y;       // double[NP] (zero past N)
+    int RY;         // double[N]
+    int P;          // float4[N] {xf, yf, rotYf, 0}
+    int CPH;        // float[NP] -cos(phi_i): FocalPoint terms
+    int RMX, RMA;   // float[2][NP] -(row max), int[2][NP] argmax: symmetry rows, cur/proposed
+    int CLA;        // float4[C] clearance boxes at their source objects
+    int NZ;         // uint64[C][W] non-zero Clearance pairs (row = clearance, bit = object)
+    int SAM, SAMB;  // uint32[SW] non-zero SurfaceArea entries (C clearances then N objects), backup
+    int RPW, RANG;  // double[max(R, NP)] negated PairWise / PairWiseAngle terms (zero past R)
+    int LCL, LSA;   // float[cap] compacted negated Clearance / SurfaceArea terms (zero filled)
+    int AUX;        // per-chain scalars (backups, current costs)
+    int W, SW;      // words per NZ row, SAM words
+    int cap_cl, cap_sa;
+    int stride;     // bytes per chain
+};
+
+inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h_rel,
+                             int& h_frz, int& h_room);
+
+inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
+    DeltaLds l;
+    const int np = (n + 1 + 3) & ~3;
+    l.NP = np;
+    int h = room_header(n, c, r, l.h_obj, l.h_clr, l.h_rel, l.h_frz, l.h_room);
+    l.h_area = h; h += round16(4 * np);
+    l.h_ones = h; h += round16(4 * np);
+    l.h_zero = h; h += round16(8 * np);
+    l.hdr = h;
+    l.W = (n + 63) / 64;
+    l.SW = (c + n + 31) / 32;
+    l.cap_cl = 2 * np < 32 ? 32 : 2 * np;
+    l.cap_sa = np < 32 ? 32 : np;
+    const int nrp = r > np ? ((r + 3) & ~3) : np;
+    int o = 0;
+    l.X = o;    o += 8 * np;
+    l.Y = o;    o += 8 * np;
+    l.RY = o;   o += round16(8 * n);
+    l.P = o;    o += 16 * n;
+    l.CPH = o;  o += 4 * np;
+    l.RMX = o;  o += 4 * 2 * np;
+    l.RMA = o;  o += round16(4 * 2 * np);
+    l.CLA = o;  o += 16 * (c > 0 ? c : 1);
+    l.NZ = o;   o += 8 * l.W * (c > 0 ? c : 1);
+    l.RPW = o;  o += 8 * nrp;
+    l.RANG = o; o += round16(8 * nrp);
+    l.SAM = o;  o += 4 * l.SW;
+    l.SAMB = o; o += round16(4 * l.SW);
+    l.LCL = o;  o += 4 * l.cap_cl;
+    l.LSA = o;  o += round16(4 * l.cap_sa);
+    l.AUX = o;  o += 192;
+    o = round16(o);
+    if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
+    l.stride = o;
+    return l;
+}
+
+inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h_rel,
+                             int& h_frz, int& h_room) {
+    int h = 0;
+    h_obj = h; h += round16((int)sizeof(ObjConst) * n);
+    h_clr = h; h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
+    h_rel = h; h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
+    h_frz = h; h += round16(n + 1);
+    h_room = h; h += round16((int)sizeof(DevRoom));
+    return h;
+}
+
 inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L) {
     ChainLds l;
-    int h = 0;
-    l.h_obj = h; h += round16((int)sizeof(ObjConst) * n);
-    l.h_clr = h; h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
-    l.h_rel = h; h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
-    l.h_frz = h; h += round16(n + 1);
-    l.h_room = h; h += round16((int)sizeof(DevRoom));
-    l.hdr = h;
+    l.hdr = room_header(n, c, r, l.h_obj, l.h_clr, l.h_rel, l.h_frz, l.h_room);
     int o = 0;
     l.P = o;   o += round16(16 * n);
     l.RY = o;  o += round16(8 * n);

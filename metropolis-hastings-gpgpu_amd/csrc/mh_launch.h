@@ -1,5 +1,5 @@
 // mh_launch.h -- launch interface between the host library (mh_abi.cpp) and the HIP kernels
-// (mh_chain.hip).
+// (mh_chain.hip: full evaluation; mh_delta.hip: incremental step).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,6 +28,7 @@ struct LaunchArgs {
     uint64_t seed;
     int iterations;
     ChainLds lay;
+    DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
 };
 
 int choose_lanes(int n);
@@ -35,8 +36,11 @@ int choose_npl(int n, int L);
 int max_npl();
 size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg);
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
+size_t delta_lds_bytes(const DeltaLds& lay, int L, int waves_per_wg);
+hipError_t launch_delta(const LaunchArgs& a, int L, int waves_per_wg, hipStream_t s);
 hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
                           int64_t chain_offset, mh_summary* out, hipStream_t s);
+hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hipStream_t s);
 hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
                       float* nrm, hipStream_t s);
 

@@ -137,6 +137,35 @@ def test_chains_match_oracle(mh, orc, hiplib, kind, n, chains, steps):
     assert mean_rel <= REL_TOL
 
 
+@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("kind,n,chains,steps", [
+    ("main", 32, 128, 300),
+    ("frozen", 16, 128, 400),
+    ("wrap", 24, 96, 400),
+    ("syn", 2, 64, 300),
+    ("syn", 9, 128, 500),
+    ("syn", 64, 64, 600),
+    ("syn", 100, 16, 120),
+])
+def test_chains_match_oracle_each_step_kernel(mh, orc, hiplib, monkeypatch, step, kind, n,
+                                              chains, steps):
+    """Both step kernels (MH_DELTA=1: incremental evaluation, mh_delta.hip; MH_DELTA=0: full
+    evaluation, mh_chain.hip) against the oracle, whichever is the default for N."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    room = _room(mh, kind, n)
+    seed = 7000 + n
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
+    same = np.all(pts.view(np.uint32) == ref_pts.view(np.uint32), axis=(1, 2)) & np.all(
+        costs.view(np.uint32) == ref_costs.view(np.uint32), axis=1)
+    print(f"{step} {kind} N={n}: {same.mean() * 100:.2f}% of chains bit-identical")
+    assert same.mean() >= 0.99
+
+
 def test_chains_over_launch_chunks(mh, orc, hiplib):
     """1200 steps span two launches (1000 steps per launch): resumption is exact."""
     room = mh.synthetic_room(8)
@@ -215,14 +244,17 @@ def test_full_size_config3_properties(mh, orc, hiplib):
         assert np.array_equal(costs[cid].view(np.uint32), rc[0].view(np.uint32)), cid
 
 
+@pytest.mark.parametrize("step", ["incremental", "full"])
 @pytest.mark.parametrize("n,chains,steps", [(64, 65536, 400), (20, 16384, 1500),
                                              (256, 8192, 200), (5, 4096, 3000)])
-def test_running_costs_equal_fresh_evaluation(mh, hiplib, n, chains, steps):
+def test_running_costs_equal_fresh_evaluation(mh, hiplib, monkeypatch, step, n, chains, steps):
     """Size-independent property of the incremental evaluation: after many accepted proposals,
     the costs every chain carries for its current state (symmetry row maxima updated
     incrementally) equal a full re-evaluation of that state, bit for bit, on every chain."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
     room = mh.synthetic_room(n)
     with mh.Session(room, chains, seed=77 + n) as s:
+        assert s.step_kernel()[2] == step
         s.run(steps)
         s.finalize()
         _, fresh = s.download()
@@ -263,3 +295,26 @@ def test_golden_rng_hip(mh, hiplib, case):
     assert [int(x) for x in u] == case["u32"]
     assert [int(x) for x in f.view(np.uint32)] == case["uniform_bits"]
     assert [int(x) for x in g.view(np.uint32)] == case["normal_bits"]
+
+
+@pytest.mark.parametrize("L", [8, 16, 32, 64])
+def test_group_collectives(mh, hiplib, L):
+    """DPP / permlane group reductions and scans against numpy, with ties and negative values."""
+    rng = np.random.default_rng(L)
+    for trial in range(6):
+        v = rng.normal(size=64).astype(np.float32)
+        if trial % 2:
+            v = np.round(v * 2) / 2  # many exact ties
+        iv = rng.integers(-5, 9, size=64).astype(np.int32)
+        got = mh.debug_collectives(L, v, iv)
+        for g in range(64 // L):
+            sl = slice(g * L, (g + 1) * L)
+            vg, ig = v[sl], iv[sl]
+            srt = np.sort(vg)[::-1]
+            j = int(np.flatnonzero(vg == srt[0])[0])
+            assert np.all(got["m1"][sl] == srt[0]) and np.all(got["m2"][sl] == srt[1])
+            assert np.all(got["j1"][sl] == j) and np.all(got["arg"][sl] == j)
+            assert np.all(got["max"][sl] == srt[0])
+            assert np.array_equal(got["scan"][sl], np.concatenate([[0], np.cumsum(ig)[:-1]]))
+            assert np.all(got["total"][sl] == ig.sum())
+            assert np.all(got["imax"][sl] == ig.max()) and np.all(got["isum"][sl] == ig.sum())

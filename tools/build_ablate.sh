@@ -11,10 +11,11 @@ C=metropolis-hastings-gpgpu_amd/csrc
 for M in "$@"; do
   case "$M" in
     stamps) DEF=-DMH_STAMPS=1 ;;
+    counts) DEF=-DMH_STAMPS=2 ;;
     dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
     *) DEF=-DMH_ABLATE=$M ;;
   esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
-    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
+    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_delta.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
 done
 wait

@@ -13,6 +13,8 @@ sys.path.insert(0, str(ROOT))
 os.environ.setdefault("MH_LIB", str(ROOT / "ablate" / "libmhgpu_stamps.so"))
 import __graft_entry__ as graft  # noqa: E402
 
+DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
+                "term lists", "replay", "accept/restore", "-"]
 PHASES = ["propose", "A per-object", "B symmetry", "C ordered sums", "D surface area",
           "E clearance", "F pairwise/angle", "accept/undo"]
 
@@ -28,12 +30,23 @@ def main():
         s.finalize()
         s.summary()
         lanes, cpw = s.geometry()
-    out = (C.c_ulonglong * 8)()
-    assert lib.mh_debug_phase_cycles(out) == 0
-    tot = sum(out)
-    print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes}")
-    for name, v in zip(PHASES, out):
-        print(f"  {name:18s} {100.0 * v / tot:6.2f}%   {v / (chains * iters):10.1f} cycles/chain-step")
+    out = (C.c_ulonglong * 12)()
+    delta = hasattr(lib, "mh_debug_delta_cycles") and os.environ.get("MH_DELTA", "1") != "0" and n > 8
+    if delta:  # incremental step kernel: per-wavefront stamps, 64/lanes chains per wavefront
+        assert lib.mh_debug_delta_cycles(out) == 0
+        names, per = DELTA_PHASES, chains * iters / (64 // lanes)
+        unit = "cycles/wave-step"
+    else:
+        assert lib.mh_debug_phase_cycles(out) == 0
+        names, per, unit = PHASES, chains * iters, "cycles/chain-step"
+    tot = sum(out[:8])
+    print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes} delta={delta}")
+    for name, v in zip(names, out[:8]):
+        print(f"  {name:18s} {100.0 * v / tot:6.2f}%   {v / per:10.1f} {unit}")
+    if delta:
+        steps = chains * iters
+        print(f"  mean Clearance list {out[8] / steps:.2f}, SurfaceArea list {out[9] / steps:.2f}, "
+              f"overflow fractions {out[10] / steps:.4f} / {out[11] / steps:.4f}")
 
 
 if __name__ == "__main__":
