@@ -65,8 +65,8 @@ struct ChainPtrs {
     const RelConst* relc;
     ObjP* P;
     double* RY;
-    double* OSD;      // [N][2] per-object double terms of the dense ordered sums (px, py)
-    float* OSF;       // [N][2] per-object float terms (-cos phi, -row max)
+    double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
+    float *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max)
     float* LCL;       // compacted non-zero Clearance terms (floats), capacity 2L
     double* LPW;      // compacted non-zero PairWise / Angle terms, capacity lst_r each
     double* LANG;
@@ -99,14 +99,17 @@ __device__ __forceinline__ void list_flush(const T* buf, int& cnt, double& acc, 
     wave_sync();
 }
 
-// Appends, in lane order, the value of every lane whose `nz` is set.
+// Appends, in lane order, the value of every lane whose `nz` is set (folding the list into its
+// owner's accumulator first only if these values would not fit).
 template <int L, typename T>
 __device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& acc, bool owner,
                                             bool to_float, T v, bool nz, int r, int gbase) {
-    if (cnt + L > cap) list_flush(buf, cnt, acc, owner, to_float);
     const uint64_t b = group_ballot<L>(nz, gbase);
+    const int add = __builtin_popcountll(b);
+    if (add == 0) return;
+    if (cnt + add > cap) list_flush(buf, cnt, acc, owner, to_float);
     if (nz) buf[cnt + __builtin_popcountll(b & ((1ull << r) - 1ull))] = v;
-    cnt += __builtin_popcountll(b);
+    cnt += add;
 }
 
 // PairWiseCosts / PairWiseAngleCosts terms of relationship q (mh_common.h).
@@ -424,10 +427,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
         if (i < n) {
-            ch.OSD[2 * i] = px[m];
-            ch.OSD[2 * i + 1] = py[m];
-            ch.OSF[2 * i] = -cph[m];
-            ch.OSF[2 * i + 1] = -sym.mx[m];
+            ch.PX[i] = px[m];
+            ch.PY[i] = py[m];
+            ch.CPHF[i] = -cph[m];
+            ch.RMXF[i] = -sym.mx[m];
         }
     }
     // SurfaceAreaCosts: clearances (quirk box at cfg[i]) first, then objects (:453-480);
@@ -453,8 +456,11 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     float4 offb[NPL];
 #pragma unroll
     for (int m = 0; m < NPL; ++m) offb[m] = (m * L + r < n) ? ch.OFF[m * L + r] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int ci = 0; ci < ((MH_ABLATE & 8) ? 0 : c); ++ci) {
-        const float4 A = ch.CLA[ci];
+    const int cend = (MH_ABLATE & 8) ? 0 : c;
+    float4 A_next = cend > 0 ? ch.CLA[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ci = 0; ci < cend; ++ci) {
+        const float4 A = A_next;  // box ci; box ci + 1 is in flight during the appends
+        if (ci + 1 < cend) A_next = ch.CLA[ci + 1];
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
             if (m * L >= n) break;
@@ -494,54 +500,62 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // The replay: lane k walks its own sequence in the reference's order. Lanes 0/1: the
     // VisualBalance products (double terms, float accumulators); 2: -cos phi (float terms,
     // double accumulator); 3: -row max (float, float); 4: Clearance list (float, float);
-    // 6/7: PairWise / Angle lists (double, double).
+    // 6/7: PairWise / Angle lists (double, double). Every sequence is zero-padded to a multiple
+    // of four terms; a lane reads four at a time (two ds_read_b128 of doubles or one of
+    // floats) and keeps both a double- and a float-rounded walk of the same terms.
+    for (int q = cnt_cl + r; q < ((cnt_cl + 3) & ~3); q += L) ch.LCL[q] = 0.0f;
+    for (int q = cnt_pw + r; q < ((cnt_pw + 3) & ~3); q += L) ch.LPW[q] = 0.0;
+    for (int q = cnt_ang + r; q < ((cnt_ang + 3) & ~3); q += L) ch.LANG[q] = 0.0;
     wave_sync();
     const double acc0 = acc;
     for (int rep = 0; rep < MH_REPS(32); ++rep) {
         MH_CLOBBER();
-        acc = acc0;
         const int k = r;
+        const double* dsrc = ch.PX;
+        const float* fsrc = ch.CPHF;
         int len = 0;
-        const double* dsrc = ch.OSD;
-        const float* fsrc = ch.OSF;
-        int dstride = 0, fstride = 0;
-        bool from_float = false;
+        const bool is_d = (k == 0 || k == 1 || k == 6 || k == 7);
         if (k == 0 || k == 1) {
-            len = (MH_ABLATE & 4) ? 0 : n;
-            dsrc = ch.OSD + k;
-            dstride = 2;
+            dsrc = k == 0 ? ch.PX : ch.PY;
+            len = n;
         } else if (k == 2 || k == 3) {
-            len = (MH_ABLATE & 4) ? 0 : n;
-            fsrc = ch.OSF + (k - 2);
-            fstride = 2;
-            from_float = true;
+            fsrc = k == 2 ? ch.CPHF : ch.RMXF;
+            len = n;
         } else if (k == 4) {
-            len = cnt_cl;
             fsrc = ch.LCL;
-            fstride = 1;
-            from_float = true;
+            len = cnt_cl;
         } else if (k == 6 || k == 7) {
-            len = k == 6 ? cnt_pw : cnt_ang;
             dsrc = k == 6 ? ch.LPW : ch.LANG;
-            dstride = 1;
+            len = k == 6 ? cnt_pw : cnt_ang;
         }
-        const int steps = max(n, max(cnt_cl, max(cnt_pw, cnt_ang)));
-        // Terms past a lane's length read as +0 (acc + 0 == acc: an accumulator is never -0),
-        // so eight loads can be in flight ahead of the dependent adds.
-        for (int l0 = 0; l0 < steps; l0 += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int l = l0 + u;
-                v[u] = (l < len) ? (from_float ? (double)fsrc[l * fstride] : dsrc[l * dstride])
-                                 : 0.0;
+        len = (len + 3) & ~3;
+        const int steps = group_max<L>(len);
+        double accd = acc0, accf = acc0;
+        for (int l0 = 0; l0 < steps; l0 += 4) {
+            double v[4] = {0.0, 0.0, 0.0, 0.0};
+            if (l0 < len) {
+                if (is_d) {
+                    const double2 a0 = *reinterpret_cast<const double2*>(dsrc + l0);
+                    const double2 a1 = *reinterpret_cast<const double2*>(dsrc + l0 + 2);
+                    v[0] = a0.x;
+                    v[1] = a0.y;
+                    v[2] = a1.x;
+                    v[3] = a1.y;
+                } else {
+                    const float4 f = *reinterpret_cast<const float4*>(fsrc + l0);
+                    v[0] = f.x;
+                    v[1] = f.y;
+                    v[2] = f.z;
+                    v[3] = f.w;
+                }
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const double t = acc + v[u];
-                acc = acc_float ? (double)(float)t : t;
+            for (int u = 0; u < 4; ++u) {
+                accd = accd + v[u];
+                accf = (double)(float)(accf + v[u]);
             }
         }
+        acc = acc_float ? accf : accd;
     }
     const float nx = (float)grp_get<L>(acc, 0, gbase);
     const float ny = (float)grp_get<L>(acc, 1, gbase);
@@ -734,8 +748,10 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     ch.relc = relc_l;
     ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
     ch.RY = reinterpret_cast<double*>(base + a.lay.RY);
-    ch.OSD = reinterpret_cast<double*>(base + a.lay.OSD);
-    ch.OSF = reinterpret_cast<float*>(base + a.lay.OSF);
+    ch.PX = reinterpret_cast<double*>(base + a.lay.PX);
+    ch.PY = reinterpret_cast<double*>(base + a.lay.PY);
+    ch.CPHF = reinterpret_cast<float*>(base + a.lay.CPHF);
+    ch.RMXF = reinterpret_cast<float*>(base + a.lay.RMXF);
     ch.LCL = reinterpret_cast<float*>(base + a.lay.LCL);
     ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
     ch.lst_r = a.lay.lst_r;
@@ -747,6 +763,13 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
     ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
 
+    // Zero the dense replay streams past N (never written afterwards).
+    for (int i = n + r; i < a.lay.N4; i += L) {
+        ch.PX[i] = 0.0;
+        ch.PY[i] = 0.0;
+        ch.CPHF[i] = 0.0f;
+        ch.RMXF[i] = 0.0f;
+    }
     // Stage the configuration into LDS.
     const double* src;
     if constexpr (OP == OP_INIT) src = a.cfg;

@@ -99,11 +99,12 @@ struct ChainLds {
     int OFF;     // float4[N] off-limits boxes of the current configuration
     int CLA;     // float4[C] clearance boxes at their source objects
     int AUX;     // ChainAux: proposal backups and the current costs
-    int OSD;     // double[N][2] per-object VisualBalance products of the ordered sums
-    int OSF;     // float[N][2]  per-object -cos(phi) and -row max
+    int PX, PY;    // double[N4] per-object VisualBalance products (N4 = round4(N), zero past N)
+    int CPHF, RMXF;  // float[N4] per-object -cos(phi) and -row max
     int LCL;     // float[2L]    compacted non-zero Clearance terms
     int LPW;     // double[2 * lst_r] compacted non-zero PairWise then Angle terms
-    int lst_r;   // min(L, max(R, 1))
+    int lst_r;   // round4(min(L, max(R, 1)))
+    int N4;
     int stride;  // bytes per chain
 };
 
@@ -195,11 +196,14 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L) {
     l.OFF = o; o += round16(16 * n);
     l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
     l.AUX = o; o += 256;
-    l.lst_r = r < 1 ? 1 : (r < L ? r : L);
-    l.OSD = o; o += round16(16 * n);
-    l.OSF = o; o += round16(8 * n);
-    l.LCL = o; o += round16(8 * L);
-    l.LPW = o; o += round16(16 * l.lst_r);
+    l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
+    l.N4 = (n + 3) & ~3;
+    l.PX = o;   o += 8 * l.N4;
+    l.PY = o;   o += 8 * l.N4;
+    l.CPHF = o; o += 4 * l.N4;
+    l.RMXF = o; o += round16(4 * l.N4);
+    l.LCL = o;  o += round16(8 * L);
+    l.LPW = o;  o += round16(16 * l.lst_r);
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
     l.stride = o;
