@@ -89,19 +89,20 @@ def cpu_baseline(room, orc, seed: int, budget_s: float, threads: int):
                       f" ({dt:.1f} s, {threads} threads)"}
 
 
-def pmc_traffic(n_chains_per_launch: int):
-    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC pass, if present
-    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py), else None."""
+def pmc_record(n_chains_per_launch: int, step_kernel: str):
+    """The committed rocprofv3 PMC record of the step kernel (profiles/pmc_step_kernel.json,
+    written by tools/pmc_summary.py --json) if it was taken on this workload, else {}."""
     p = ROOT / "profiles" / "pmc_step_kernel.json"
     if not p.exists():
-        return None
+        return {}
     try:
         d = json.loads(p.read_text())
-        if int(d.get("chains_per_launch", -1)) != n_chains_per_launch:
-            return None
-        return float(d["hbm_bytes_per_launch"])
+        kind = "incremental" if "delta" in d.get("kernel", "") else "full"
+        if int(d.get("chains_per_launch", -1)) != n_chains_per_launch or kind != step_kernel:
+            return {}
+        return d
     except Exception:
-        return None
+        return {}
 
 
 def main() -> int:
@@ -200,6 +201,7 @@ def main() -> int:
             orc = graft.load_oracle()
             threads = max(1, min(16, os.cpu_count() or 1))
             cpu = cpu_baseline(room, orc, args.seed, args.cpu_budget, threads)
+        pmc = pmc_record(args.chains, step_kernel)
         out = {
             "metric": "MH chain-steps/sec (whole node) + mean final cost, N=64 objects",
             "value": value,
@@ -236,10 +238,15 @@ def main() -> int:
                 "peak": FP32_VECTOR_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP32_VECTOR_PEAK_TFLOPS,
-                "traffic": pmc_traffic(args.chains),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
                 "flops_per_chain_step": f,
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "hbm_frac": bytes_launch / launch_s / 1e9 / HBM_PEAK_GBS,
+                # F is the canonical full-recompute count; the executed count is
+                # the PMC VALU wavefront instructions per chain-step of this build.
+                "executed_valu_wave_insts_per_chain_step": (
+                    pmc["valu_wave_insts_per_launch"] / (args.chains * pmc["iters_per_launch"])
+                    if pmc.get("valu_wave_insts_per_launch") else None),
             },
             "cpu_baseline": cpu,
         }

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("tag_dir")
     ap.add_argument("--kernel", default="mh_kernel<64, 1, 1>")
     ap.add_argument("--chains", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=1000, help="MH steps per launch")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     c, meta = load(a.tag_dir, a.kernel)
@@ -66,6 +67,9 @@ def main():
                "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
                "fetch_size_kib": c.get("FETCH_SIZE"), "write_size_kib": c.get("WRITE_SIZE"),
                "correction": "read side = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
+               "iters_per_launch": a.iters,
+               "valu_wave_insts_per_launch": c.get("SQ_INSTS_VALU"),
+               "salu_insts_per_launch": c.get("SQ_INSTS_SALU"),
                "source": os.path.normpath(a.tag_dir)}
         with open(a.json, "w") as fh:
             json.dump(rec, fh, indent=1)
