@@ -207,7 +207,9 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
 
 struct Geometry {
     int L, npl, waves;   // full-evaluation kernel (init, final, evaluation; step when !delta)
-    mh::ChainLds lay;
+    mh::ChainLds lay;    // init / step
+    int waves_ol;
+    mh::ChainLds lay_ol; // final / evaluation (with the OffLimits boxes)
     bool delta;          // step with the incremental kernel (mh_delta.hip)
     int dL, dwaves;
     mh::DeltaLds dlay;
@@ -260,7 +262,10 @@ bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     // Four waves per workgroup while that keeps at least two workgroups per CU.
     g.waves = 4;
     while (g.waves > 1 && mh::lds_bytes(g.lay, g.L, g.waves) > 80 * 1024) g.waves >>= 1;
-    if (mh::lds_bytes(g.lay, g.L, g.waves) > (size_t)max_lds) {
+    g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
+    g.waves_ol = g.waves;
+    while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
+    if (mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > (size_t)max_lds) {
         set_error("room does not fit in LDS");
         return false;
     }
@@ -387,7 +392,9 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
 
 bool session_finalize(mh_session* s, hipStream_t st) {
     MH_TRY_HIP(hipSetDevice(s->device));
-    MH_TRY_HIP(mh::launch(mh::OP_FINAL, s->args(), s->geo.L, s->geo.npl, s->geo.waves, st));
+    mh::LaunchArgs a = s->args();
+    a.lay = s->geo.lay_ol;
+    MH_TRY_HIP(mh::launch(mh::OP_FINAL, a, s->geo.L, s->geo.npl, s->geo.waves_ol, st));
     return true;
 }
 
@@ -598,7 +605,8 @@ MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationship
         a.cfg = d_cfgs;
         a.costs = d_out;
         a.n_chains = n_cfgs;
-        fail(mh::launch(mh::OP_EVAL, a, s->geo.L, s->geo.npl, s->geo.waves, s->stream), "launch");
+        a.lay = s->geo.lay_ol;
+        fail(mh::launch(mh::OP_EVAL, a, s->geo.L, s->geo.npl, s->geo.waves_ol, s->stream), "launch");
     }
     if (ok) fail(hipStreamSynchronize(s->stream), "hipStreamSynchronize");
     if (ok) fail(hipMemcpy(out_costs, d_out, sizeof(resultCosts) * n_cfgs, hipMemcpyDeviceToHost), "hipMemcpy");

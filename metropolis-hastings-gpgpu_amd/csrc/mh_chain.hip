@@ -57,11 +57,11 @@ struct ChainAux {
     unsigned long long cyc[8];  // diagnostic: cycles per phase (writer lane)
 #endif
 };
-static_assert(sizeof(ChainAux) <= 256, "ChainAux");
+static_assert(sizeof(ChainAux) <= kChainAuxBytes, "ChainAux");
 
 struct ChainPtrs {
-    const ObjConst* objc;  // room tables, staged once per workgroup into LDS
-    const ClrConst* clrc;
+    const RectShape* objs;  // room tables, staged once per workgroup into LDS (ChainLds)
+    const RectShape* clrs;
     const RelConst* relc;
     ObjP* P;
     double* RY;
@@ -148,13 +148,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
         sao[m] = sac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n) {
-            const ObjConst oc = ch.objc[i];
+            const RectShape os = ch.objs[i];
+            const float area = __int_as_float(os.pad);
             const ObjP p = ch.P[i];
             const double x = ch.X[i], y = ch.Y[i];
             wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(ch.RY[i]) < 1e15);
             // VisualBalanceCosts products, Kernel.cu:200-201.
-            px[m] = (double)oc.area * x;
-            py[m] = (double)oc.area * y;
+            px[m] = (double)area * x;
+            py[m] = (double)area * y;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188.
             if (!(MH_ABLATE & 2)) {
                 float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
@@ -172,18 +173,18 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
             rrs[m] = rr;
             // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
-            float4 box = shape_box(oc.off, p.xf, p.yf);
-            ch.OFF[i] = box;
+            float4 box = shape_box(os, p.xf, p.yf);
+            if constexpr (WITH_OL) ch.OFF[i] = box;
             sao[m] = comp_overlaps(rm, box);
         }
         rpw[m] = rang[m] = 0.0;
         if (!(MH_ABLATE & 16) && i < rm.r) rel_terms(ch, i, rpw[m], rang[m]);
         if (i < c) {
-            const ClrConst cc = ch.clrc[i];
-            const ObjP ps = ch.P[cc.src];
-            ch.CLA[i] = shape_box(cc.shape, ps.xf, ps.yf);       // ClearanceCosts, :414-415
+            const RectShape cs = ch.clrs[i];
+            const ObjP ps = ch.P[cs.pad];
+            ch.CLA[i] = shape_box(cs, ps.xf, ps.yf);             // ClearanceCosts, :414-415
             const ObjP pi = ch.P[i];                              // SurfaceArea quirk: cfg[i], :456
-            sac[m] = comp_overlaps(rm, shape_box(cc.shape, pi.xf, pi.yf));
+            sac[m] = comp_overlaps(rm, shape_box(cs, pi.xf, pi.yf));
         }
     }
     }
@@ -455,7 +456,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     cnt_cl = 0;
     float4 offb[NPL];
 #pragma unroll
-    for (int m = 0; m < NPL; ++m) offb[m] = (m * L + r < n) ? ch.OFF[m * L + r] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < NPL; ++m) {  // this lane's off-limits boxes (recomputed: no LDS copy)
+        const int j = m * L + r;
+        offb[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < n) {
+            const ObjP p = ch.P[j];
+            offb[m] = shape_box(ch.objs[j], p.xf, p.yf);
+        }
+    }
     const int cend = (MH_ABLATE & 8) ? 0 : c;
     float4 A_next = cend > 0 ? ch.CLA[0] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int ci = 0; ci < cend; ++ci) {
@@ -715,8 +723,14 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
 
 // ---- the kernel ---------------------------------------------------------------------------
 
+#ifdef MH_WAVES_PER_EU  // occupancy experiments: ask the register allocator for more waves
+#define MH_OCC __attribute__((amdgpu_waves_per_eu(MH_WAVES_PER_EU, 8)))
+#else
+#define MH_OCC
+#endif
+
 template <int L, int NPL, int OP>
-__global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
+__global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / L;
     const int n = a.rm.n;
@@ -728,12 +742,20 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     const int waves_per_wg = blockDim.x >> 6;
 
     // Room tables: staged once per workgroup (the chain loop then never touches global memory).
-    ObjConst* objc_l = reinterpret_cast<ObjConst*>(lds + a.lay.h_obj);
-    ClrConst* clrc_l = reinterpret_cast<ClrConst*>(lds + a.lay.h_clr);
+    RectShape* objs_l = reinterpret_cast<RectShape*>(lds + a.lay.h_obj);
+    RectShape* clrs_l = reinterpret_cast<RectShape*>(lds + a.lay.h_clr);
     RelConst* relc_l = reinterpret_cast<RelConst*>(lds + a.lay.h_rel);
     unsigned char* frozen = lds + a.lay.h_frz;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) objc_l[i] = a.objc[i];
-    for (int i = threadIdx.x; i < a.rm.c; i += blockDim.x) clrc_l[i] = a.clrc[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        RectShape s = a.objc[i].off;
+        s.pad = __float_as_int(a.objc[i].area);
+        objs_l[i] = s;
+    }
+    for (int i = threadIdx.x; i < a.rm.c; i += blockDim.x) {
+        RectShape s = a.clrc[i].shape;
+        s.pad = a.clrc[i].src;
+        clrs_l[i] = s;
+    }
     for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) relc_l[i] = a.relc[i];
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     __syncthreads();
@@ -743,8 +765,8 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
 
     unsigned char* base = lds + a.lay.hdr + (wave * G + g) * a.lay.stride;
     ChainPtrs ch;
-    ch.objc = objc_l;
-    ch.clrc = clrc_l;
+    ch.objs = objs_l;
+    ch.clrs = clrs_l;
     ch.relc = relc_l;
     ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
     ch.RY = reinterpret_cast<double*>(base + a.lay.RY);
@@ -759,7 +781,7 @@ __global__ void __launch_bounds__(256) mh_kernel(LaunchArgs a) {
     ch.X = reinterpret_cast<double*>(base + a.lay.X);
     ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
-    ch.OFF = reinterpret_cast<float4*>(base + a.lay.OFF);
+    ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
     ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
 

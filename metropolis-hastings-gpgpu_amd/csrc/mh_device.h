@@ -85,18 +85,27 @@ static_assert(sizeof(ChainMeta) == 64, "ChainMeta");
 // x, y, rotY enter the costs; z, rotX, rotZ (contiguous, F_Z..F_RZ) never do.
 enum { F_X = 0, F_Y = 1, F_RY = 2, F_Z = 3, F_RX = 4, F_RZ = 5, F_COUNT = 6 };
 
-// LDS carve-up. One workgroup = WAVES waves; each wave holds G = 64/L chains.
+// Per-chain scalars of the full-evaluation kernel (mh_chain.hip ChainAux), bytes.
+#if defined(MH_STAMPS) && MH_STAMPS
+constexpr int kChainAuxBytes = 192;
+#else
+constexpr int kChainAuxBytes = 128;
+#endif
+
+// LDS carve-up of the full-evaluation kernel. One workgroup = WAVES waves; each wave holds
+// G = 64/L chains. The room tables are kept as 40-byte RectShape records: an object's
+// off-limits rectangle with its area in .pad, a clearance's rectangle with its source in .pad.
 struct ChainLds {
     int hdr;     // bytes of the per-workgroup header: room tables + frozen flags
-    int h_obj;   // ObjConst[N] within the header
-    int h_clr;   // ClrConst[C]
+    int h_obj;   // RectShape[N] within the header (pad = area bits)
+    int h_clr;   // RectShape[C] (pad = source object)
     int h_rel;   // RelConst[R]
     int h_frz;   // unsigned char[N + 1] frozen flags (index N counts as frozen)
     int h_room;  // DevRoom copy (read by the out-of-line cost evaluation)
     int P;       // ObjP[N]   {float xf, yf, rotYf, pad}
     int RY;      // double[N] rotY
     int X, Y;    // double[N]   (z, rotX, rotZ never enter a cost: they stay in HBM)
-    int OFF;     // float4[N] off-limits boxes of the current configuration
+    int OFF;     // float4[N] off-limits boxes (final / evaluation passes only; -1 in the step)
     int CLA;     // float4[C] clearance boxes at their source objects
     int AUX;     // ChainAux: proposal backups and the current costs
     int PX, PY;    // double[N4] per-object VisualBalance products (N4 = round4(N), zero past N)
@@ -185,17 +194,28 @@ inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h
     return h;
 }
 
-inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L) {
+// with_off: the layout of the passes that evaluate OffLimitsCosts (final state, evaluation).
+inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off = false) {
     ChainLds l;
-    l.hdr = room_header(n, c, r, l.h_obj, l.h_clr, l.h_rel, l.h_frz, l.h_room);
+    int h = 0;
+    l.h_obj = h;  h += round16((int)sizeof(RectShape) * n);
+    l.h_clr = h;  h += round16((int)sizeof(RectShape) * (c > 0 ? c : 1));
+    l.h_rel = h;  h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
+    l.h_frz = h;  h += round16(n + 1);
+    l.h_room = h; h += round16((int)sizeof(DevRoom));
+    l.hdr = h;
     int o = 0;
     l.P = o;   o += round16(16 * n);
     l.RY = o;  o += round16(8 * n);
     l.X = o;   o += round16(8 * n);
     l.Y = o;   o += round16(8 * n);
-    l.OFF = o; o += round16(16 * n);
+    l.OFF = -1;
+    if (with_off) {
+        l.OFF = o;
+        o += round16(16 * n);
+    }
     l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
-    l.AUX = o; o += 256;
+    l.AUX = o; o += kChainAuxBytes;
     l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
     l.N4 = (n + 3) & ~3;
     l.PX = o;   o += 8 * l.N4;

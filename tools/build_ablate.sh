@@ -12,6 +12,7 @@ for M in "$@"; do
   case "$M" in
     stamps) DEF=-DMH_STAMPS=1 ;;
     counts) DEF=-DMH_STAMPS=2 ;;
+    wpe*) DEF=-DMH_WAVES_PER_EU=${M#wpe} ;;
     dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
     *) DEF=-DMH_ABLATE=$M ;;
   esac
