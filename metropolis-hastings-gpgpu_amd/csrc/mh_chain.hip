@@ -537,7 +537,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             len = k == 6 ? cnt_pw : cnt_ang;
         }
         len = (len + 3) & ~3;
-        const int steps = group_max<L>(len);
+        // The Clearance list (float terms, float accumulator) usually outruns the dense sums:
+        // its part past them runs in plain fp32 below (rn_f(a + b) is the reference's float add).
+        const int len_main = (k == 4) ? min(len, a.lay.N4) : len;
+        const int steps = group_max<L>(len_main);
         double accd = acc0, accf = acc0;
         for (int l0 = 0; l0 < steps; l0 += 4) {
             double v[4] = {0.0, 0.0, 0.0, 0.0};
@@ -562,6 +565,17 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 accd = accd + v[u];
                 accf = (double)(float)(accf + v[u]);
             }
+        }
+        if (k == 4 && len > steps) {
+            float a32 = (float)accf;
+            for (int l0 = steps; l0 < len; l0 += 4) {
+                const float4 f = *reinterpret_cast<const float4*>(fsrc + l0);
+                a32 = a32 + f.x;
+                a32 = a32 + f.y;
+                a32 = a32 + f.z;
+                a32 = a32 + f.w;
+            }
+            accf = a32;
         }
         acc = acc_float ? accf : accd;
     }
