@@ -336,8 +336,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             }
         }
     }
-    // Re-scans, one row at a time across the whole group.
+    // Re-scans, one row at a time across the whole group: estimates and the top-2 reduction
+    // here; the exact value of a clear row's leader is evaluated afterwards by the row's owner
+    // lane, all rows in one pass.
     uint64_t rows[NPL];
+    int lead[NPL];
+    unsigned leadp = 0u;  // slots with a leader pending exact evaluation
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) lead[m] = -1;
     bool any_row = false;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
@@ -368,15 +374,11 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             }
         }
         group_top2<L>(t1, t2, tj);
-        float best;
-        int barg;
-        if (!exact_mode && tj >= 0 &&
-            (t2 == -INFINITY || t1 - t2 > sym_err(t1, rr) + sym_err(t2, rr))) {
-            const ObjP q = ch.P[tj];
-            const float e = sym_val_exact(q.xf, q.yf, ch.RY[tj], rx, ry, (double)rr);
-            best = fmaxf(0.0f, e);
-            barg = e > 0.0f ? tj : -1;
-        } else {
+        float best = 0.0f;
+        int barg = -1;
+        const bool clear = !exact_mode && tj >= 0 &&
+                           (t2 == -INFINITY || t1 - t2 > sym_err(t1, rr) + sym_err(t2, rr));
+        if (!clear) {
             const float thr =
                 (exact_mode || tj < 0) ? INFINITY : 2.0f * sym_err(fabsf(t1) + 1.0f, rr);
             float bv = -INFINITY;
@@ -401,12 +403,34 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         for (int m = 0; m < NPL; ++m) {
             if (m == ms) {
                 if (r == b) {
-                    sym.mx[m] = best;
-                    sym.arg[m] = barg;
+                    if (clear) {
+                        lead[m] = tj;
+                        leadp |= 1u << m;
+                    } else {
+                        sym.mx[m] = best;
+                        sym.arg[m] = barg;
+                    }
                 }
                 rows[m] &= rows[m] - 1;
             }
             any_row |= rows[m] != 0;
+        }
+    }
+    while (__ballot(leadp != 0u)) {
+        if (leadp) {
+            const int ms = __builtin_ctz(leadp);
+            leadp &= leadp - 1u;
+            const int j = sel<NPL>(lead, ms);
+            const ObjP q = ch.P[j];
+            const float e = sym_val_exact(q.xf, q.yf, ch.RY[j], sel<NPL>(rxs, ms),
+                                          sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) {
+                if (m == ms) {
+                    sym.mx[m] = fmaxf(0.0f, e);
+                    sym.arg[m] = e > 0.0f ? j : -1;
+                }
+            }
         }
     }
     }
