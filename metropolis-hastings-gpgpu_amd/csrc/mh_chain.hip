@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.LCL = reinterpret_cast<float*>(base + a.lay.LCL);
     ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
     ch.lst_r = a.lay.lst_r;
-    ch.LANG = ch.LPW + ch.lst_r;
+    ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
     ch.X = reinterpret_cast<double*>(base + a.lay.X);
     ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;

@@ -76,7 +76,9 @@ static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, un
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
     const double rad = sqrt(-2.0 * log(u1));
     const double ang = 6.283185307179586 * u2;
-    return make_float2((float)(rad * sin(ang)), (float)(rad * cos(ang)));
+    double s, c;
+    sincos(ang, &s, &c);  // OCML's sin and cos share one argument reduction
+    return make_float2((float)(rad * s), (float)(rad * c));
 }
 
 // rocRAND Philox4x32-10 stream of one chain. Words are taken a block of four at a time with

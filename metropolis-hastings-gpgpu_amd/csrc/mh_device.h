@@ -111,13 +111,23 @@ struct ChainLds {
     int PX, PY;    // double[N4] per-object VisualBalance products (N4 = round4(N), zero past N)
     int CPHF, RMXF;  // float[N4] per-object -cos(phi) and -row max
     int LCL;     // float[2L]    compacted non-zero Clearance terms
-    int LPW;     // double[2 * lst_r] compacted non-zero PairWise then Angle terms
+    int LPW, LANG;  // double[lst_r] compacted non-zero PairWise / Angle terms
     int lst_r;   // round4(min(L, max(R, 1)))
     int N4;
     int stride;  // bytes per chain
 };
 
 inline MH_HD int round16(int v) { return (v + 15) & ~15; }
+
+// Next 16-byte-aligned offset >= o whose 16-byte bank slot (offset / 16 mod 16) is not in
+// *used; marks it. Arrays that the lanes of one wave read with the same instruction at the
+// same index then start on different LDS banks (bank = address / 4 mod 64).
+inline MH_HD int bank_place(int o, unsigned* used) {
+    o = round16(o);
+    for (int k = 0; k < 16 && ((*used >> ((o >> 4) & 15)) & 1u); ++k) o += 16;
+    *used |= 1u << ((o >> 4) & 15);
+    return o;
+}
 
 // LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables as in
 // ChainLds plus three replay streams (areas, ones, zeros), then per chain the configuration and
@@ -218,12 +228,16 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off 
     l.AUX = o; o += kChainAuxBytes;
     l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
     l.N4 = (n + 3) & ~3;
-    l.PX = o;   o += 8 * l.N4;
-    l.PY = o;   o += 8 * l.N4;
-    l.CPHF = o; o += 4 * l.N4;
-    l.RMXF = o; o += round16(4 * l.N4);
-    l.LCL = o;  o += round16(8 * L);
-    l.LPW = o;  o += round16(16 * l.lst_r);
+    // The replay's streams: lanes 0, 1, 6, 7 read PX, PY, LPW, LANG with one instruction,
+    // lanes 2, 3, 4 read CPHF, RMXF, LCL with another -- each set on distinct banks.
+    unsigned dslots = 0u, fslots = 0u;
+    l.PX = bank_place(o, &dslots);   o = l.PX + 8 * l.N4;
+    l.PY = bank_place(o, &dslots);   o = l.PY + 8 * l.N4;
+    l.CPHF = bank_place(o, &fslots); o = l.CPHF + 4 * l.N4;
+    l.RMXF = bank_place(o, &fslots); o = l.RMXF + 4 * l.N4;
+    l.LCL = bank_place(o, &fslots);  o = l.LCL + 8 * L;
+    l.LPW = bank_place(o, &dslots);  o = l.LPW + 8 * l.lst_r;
+    l.LANG = bank_place(o, &dslots); o = l.LANG + 8 * l.lst_r;
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
     l.stride = o;
