@@ -112,7 +112,32 @@ __device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& a
     cnt += add;
 }
 
-// PairWiseCosts / PairWiseAngleCosts terms of relationship q (mh_common.h).
+// Appends K values per lane in order k = 0..K-1 (each in lane order): one overflow test and
+// one count update for the batch.
+template <int L, int K, typename T>
+__device__ __forceinline__ void list_append_n(T* buf, int cap, int& cnt, double& acc, bool owner,
+                                              bool to_float, const T (&v)[K],
+                                              const bool (&nz)[K], int r, int gbase) {
+    uint64_t b[K];
+    int add = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        b[k] = group_ballot<L>(nz[k], gbase);
+        add += __builtin_popcountll(b[k]);
+    }
+    if (add == 0) return;
+    if (cnt + add > cap) list_flush(buf, cnt, acc, owner, to_float);
+    const uint64_t below = (1ull << r) - 1ull;
+    int pos = cnt;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (nz[k]) buf[pos + __builtin_popcountll(b[k] & below)] = v[k];
+        pos += __builtin_popcountll(b[k]);
+    }
+    cnt = pos;
+}
+
+// PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q (mh_common.h).
 __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tpw, double& tang) {
     rel_terms(ch.relc[q], ch.P, tpw, tang);
 }
@@ -489,13 +514,36 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         }
     }
     const int cend = (MH_ABLATE & 8) ? 0 : c;
-    float4 A_next = cend > 0 ? ch.CLA[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int ci = 0; ci < cend; ++ci) {
-        const float4 A = A_next;  // box ci; box ci + 1 is in flight during the appends
-        if (ci + 1 < cend) A_next = ch.CLA[ci + 1];
+    // One object per lane: two clearances per iteration (boxes for the next two in flight),
+    // one overflow test and count update per pair (a pair appends at most 2L <= capacity
+    // terms). Otherwise one clearance per iteration.
+    float4 A0n = cend > 0 ? ch.CLA[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 A1n = cend > 1 ? ch.CLA[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    int ci = 0;
+    for (; NPL == 1 && ci + 1 < cend; ci += 2) {
+        const float4 A0 = A0n, A1 = A1n;
+        if (ci + 2 < cend) A0n = ch.CLA[ci + 2];
+        if (ci + 3 < cend) A1n = ch.CLA[ci + 3];
+        float v[2 * NPL];
+        bool nz[2 * NPL];
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
-            if (m * L >= n) break;
+            const bool own = m * L + r < n;
+            const float a0 = own ? overlap(A0, offb[m]) : 0.0f;
+            const float a1 = own ? overlap(A1, offb[m]) : 0.0f;
+            v[m] = -a0;
+            nz[m] = a0 != 0.0f;
+            v[NPL + m] = -a1;
+            nz[NPL + m] = a1 != 0.0f;
+        }
+        list_append_n<L, 2 * NPL, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, v, nz, r,
+                                         gbase);
+    }
+    for (; ci < cend; ++ci) {
+        const float4 A = A0n;  // box ci; box ci + 1 is in flight during the appends
+        if (ci + 1 < cend) A0n = ch.CLA[ci + 1];
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
             const int j = m * L + r;
             const float ar = (j < n) ? overlap(A, offb[m]) : 0.0f;
             list_append<L, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, -ar, ar != 0.0f, r,
