@@ -148,6 +148,31 @@ MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStr
                                    vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg,
                                    uint64_t seed);
 
+/* Options of the extended entry points. */
+typedef enum mh_track_best {
+    MH_TRACK_OFF = 0,     /* output = each chain's final current state (Kernel.cu:834-850) */
+    MH_TRACK_LOWEST = 1,  /* output = the lowest-totalCosts configuration a chain proposed,
+                             the reference's commented-out cfgBest (Kernel.cu:779-782, 808-816,
+                             840-860: `starCosts->totalCosts < bestCosts->totalCosts`) */
+    MH_TRACK_HIGHEST = 2  /* the same with `>`: the direction Accept climbs (Kernel.cu:706-713) */
+} mh_track_best;
+
+typedef struct mh_options {
+    uint64_t seed;       /* Philox4x32-10 key; chain c draws subsequence c */
+    int32_t track_best;  /* mh_track_best. The initial configuration is the first best; every
+                            proposal (accepted or not) is compared before the accept test; ties
+                            keep the earlier one. */
+    int32_t reserved[5]; /* must be zero */
+} mh_options;
+
+/* KernelWrapper with options (NULL = KernelWrapper's defaults with seed $MH_SEED/time). With
+ * track_best != MH_TRACK_OFF, result[i] holds chain i's best configuration and its eight cost
+ * components (OffLimits included, as bestCosts would hold them). */
+MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                               positionAndRotation* cfg, rectangle* clearances,
+                               rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
+                               Surface* srf, gpuConfig* gpuCfg, const mh_options* opts);
+
 /* Frees a KernelWrapper result (the points block and the array). NULL is a no-op. */
 MH_API void KernelFreeResult(result* res);
 
@@ -186,6 +211,17 @@ MH_API mh_session* mh_session_create(const relationshipStruct* rss,
                                      const vertex* surfaceRectangle, const Surface* srf,
                                      int device, int64_t n_chains, int64_t chain_offset,
                                      uint64_t seed);
+
+/* mh_session_create with options (opts->seed replaces `seed`). With track_best on, every chain
+ * keeps its best configuration on the device, and mh_session_finalize / download / summary
+ * report the best configurations instead of the current ones. */
+MH_API mh_session* mh_session_create_ex(const relationshipStruct* rss,
+                                        const relationshipAngleStruct* rsa,
+                                        const positionAndRotation* cfg,
+                                        const rectangle* clearances, const rectangle* offlimits,
+                                        const vertex* vertices, const vertex* surfaceRectangle,
+                                        const Surface* srf, int device, int64_t n_chains,
+                                        int64_t chain_offset, const mh_options* opts);
 
 /* Enqueues `iterations` MH steps for every chain on `stream` (a hipStream_t; NULL = the
  * session's own stream). Chains resume exactly: k runs of m steps == one run of k*m steps. */
@@ -261,5 +297,6 @@ MH_STATIC_ASSERT(sizeof(resultCosts) == 32, "resultCosts");
 MH_STATIC_ASSERT(sizeof(result) == 40, "result");
 MH_STATIC_ASSERT(offsetof(result, costs) == 8, "result.costs");
 MH_STATIC_ASSERT(sizeof(mh_summary) == 40, "mh_summary");
+MH_STATIC_ASSERT(sizeof(mh_options) == 32, "mh_options");
 
 #endif /* MH_KERNEL_H_ */

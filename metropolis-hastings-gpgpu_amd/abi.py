@@ -84,6 +84,12 @@ class mh_summary(C.Structure):
                 ("best_chain", C.c_int64), ("n_chains", C.c_int64), ("accepted", C.c_int64)]
 
 
+class mh_options(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+MH_TRACK_OFF, MH_TRACK_LOWEST, MH_TRACK_HIGHEST = 0, 1, 2
+
 STRUCT_LAYOUT = {  # (size, {field: offset}) as static_assert-ed in include/mh_kernel.h
     vertex: (24, {}),
     rectangle: (20, {}),
@@ -98,14 +104,16 @@ STRUCT_LAYOUT = {  # (size, {field: offset}) as static_assert-ed in include/mh_k
     resultCosts: (32, {}),
     result: (40, {"costs": 8}),
     mh_summary: (40, {}),
+    mh_options: (32, {"track_best": 8}),
 }
 
 COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointCosts",
                "SymmetryCosts", "ClearanceCosts", "OffLimitsCosts", "SurfaceAreaCosts"]
 
 # Every symbol include/mh_kernel.h declares.
-EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelFreeResult", "KernelLastError",
-           "KernelEvaluateCosts", "mh_session_create", "mh_session_run", "mh_session_finalize",
+EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelWrapperEx", "KernelFreeResult",
+           "KernelLastError", "KernelEvaluateCosts", "mh_session_create", "mh_session_create_ex",
+           "mh_session_run", "mh_session_finalize",
            "mh_session_download", "mh_session_current_costs", "mh_session_summary", "mh_session_geometry",
            "mh_session_destroy", "mh_debug_rng", "mh_debug_collectives"]
 
@@ -134,6 +142,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.KernelWrapper.restype = P(result)
     lib.KernelWrapperSeeded.argtypes = room_args + [P(gpuConfig), C.c_uint64]
     lib.KernelWrapperSeeded.restype = P(result)
+    lib.KernelWrapperEx.argtypes = room_args + [P(gpuConfig), P(mh_options)]
+    lib.KernelWrapperEx.restype = P(result)
     lib.KernelFreeResult.argtypes = [P(result)]
     lib.KernelFreeResult.restype = None
     lib.KernelLastError.argtypes = []
@@ -145,6 +155,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.KernelEvaluateCosts.restype = C.c_int
     lib.mh_session_create.argtypes = room_args + [C.c_int, C.c_int64, C.c_int64, C.c_uint64]
     lib.mh_session_create.restype = C.c_void_p
+    lib.mh_session_create_ex.argtypes = room_args + [C.c_int, C.c_int64, C.c_int64, P(mh_options)]
+    lib.mh_session_create_ex.restype = C.c_void_p
     lib.mh_session_run.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     lib.mh_session_run.restype = C.c_int
     lib.mh_session_finalize.argtypes = [C.c_void_p, C.c_void_p]
@@ -220,12 +232,17 @@ def points_to_array(pts, count: int) -> np.ndarray:
 # ---- calls -----------------------------------------------------------------------------------
 
 def kernel_wrapper(room: Room, chains: int, iterations: int, seed: int | None = None,
-                   block_x: int = 64):
-    """Calls KernelWrapper (or KernelWrapperSeeded) exactly as the reference's caller does and
-    returns (points [chains, N, 6] float32, costs [chains, 8] float32)."""
+                   block_x: int = 64, track: int = MH_TRACK_OFF):
+    """Calls KernelWrapper (or KernelWrapperSeeded, or KernelWrapperEx when `track` is set)
+    exactly as the reference's caller does and returns (points [chains, N, 6] float32,
+    costs [chains, 8] float32)."""
     lib = load_library()
     g = gpuConfig(chains, 0, block_x, 0, 0, iterations)
-    if seed is None:
+    if track:
+        if seed is None:
+            raise ValueError("best-of-chain tracking needs an explicit seed")
+        res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh_options(seed, track)))
+    elif seed is None:
         res = lib.KernelWrapper(*room.args(), C.byref(g))
     else:
         res = lib.KernelWrapperSeeded(*room.args(), C.byref(g), C.c_uint64(seed))
@@ -289,13 +306,18 @@ def debug_collectives(L: int, v, iv):
 class Session:
     """Device-resident chains: the shard one rank owns (chain ids [offset, offset + chains))."""
 
-    def __init__(self, room: Room, chains: int, seed: int, device: int = 0, chain_offset: int = 0):
+    def __init__(self, room: Room, chains: int, seed: int, device: int = 0, chain_offset: int = 0,
+                 track: int = MH_TRACK_OFF):
         self.lib = load_library()
         self.room = room
         self.chains = chains
         self.chain_offset = chain_offset
-        h = self.lib.mh_session_create(*room.args(), device, chains, chain_offset,
-                                       C.c_uint64(seed))
+        if track:
+            h = self.lib.mh_session_create_ex(*room.args(), device, chains, chain_offset,
+                                              C.byref(mh_options(seed, track)))
+        else:
+            h = self.lib.mh_session_create(*room.args(), device, chains, chain_offset,
+                                           C.c_uint64(seed))
         if not h:
             raise MHError(last_error(self.lib))
         self.h = h

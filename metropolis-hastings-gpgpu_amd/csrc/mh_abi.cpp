@@ -23,6 +23,10 @@
 
 #include "mh_launch.h"
 
+static_assert((int)mh::TRACK_OFF == MH_TRACK_OFF && (int)mh::TRACK_LOWEST == MH_TRACK_LOWEST &&
+                  (int)mh::TRACK_HIGHEST == MH_TRACK_HIGHEST,
+              "device and ABI best-tracking modes");
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -273,6 +277,19 @@ bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     return true;
 }
 
+bool check_options(const mh_options* o) {
+    if (o->track_best < MH_TRACK_OFF || o->track_best > MH_TRACK_HIGHEST) {
+        set_error("mh_options.track_best must be MH_TRACK_OFF, MH_TRACK_LOWEST or MH_TRACK_HIGHEST");
+        return false;
+    }
+    for (int k = 0; k < 5; ++k)
+        if (o->reserved[k] != 0) {
+            set_error("mh_options.reserved must be zero");
+            return false;
+        }
+    return true;
+}
+
 uint64_t seed_from_env() {
     const char* s = getenv("MH_SEED");
     if (s && *s) return strtoull(s, nullptr, 0);
@@ -288,11 +305,13 @@ struct mh_session {
     Geometry geo{};
     int64_t n_chains = 0, chain_offset = 0;
     uint64_t seed = 0;
+    int track = mh::TRACK_OFF;
     mh::ObjConst* d_obj = nullptr;
     mh::ClrConst* d_clr = nullptr;
     mh::RelConst* d_rel = nullptr;
     double* d_cfg0 = nullptr;
     double* d_st = nullptr;
+    double* d_best = nullptr;  // [n_chains][6][N] best-of-chain configurations (track on)
     mh::ChainMeta* d_meta = nullptr;
     point* d_pts = nullptr;
     resultCosts* d_costs = nullptr;
@@ -313,6 +332,8 @@ struct mh_session {
         a.chain_offset = chain_offset;
         a.seed = seed;
         a.iterations = 0;
+        a.track = track;
+        a.best = d_best;
         a.lay = geo.lay;
         a.dlay = geo.dlay;
         return a;
@@ -332,6 +353,7 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_rel);
     (void)hipFree(s->d_cfg0);
     (void)hipFree(s->d_st);
+    (void)hipFree(s->d_best);
     (void)hipFree(s->d_meta);
     (void)hipFree(s->d_pts);
     (void)hipFree(s->d_costs);
@@ -359,6 +381,8 @@ bool session_init(mh_session* s) {
     const int64_t nc = s->n_chains > 0 ? s->n_chains : 1;
     const size_t n = (size_t)s->room.rm.n;
     MH_TRY_HIP(hipMalloc((void**)&s->d_st, sizeof(double) * mh::F_COUNT * n * nc));
+    if (s->track != mh::TRACK_OFF)
+        MH_TRY_HIP(hipMalloc((void**)&s->d_best, sizeof(double) * mh::F_COUNT * n * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_meta, sizeof(mh::ChainMeta) * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_pts, sizeof(point) * n * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_costs, sizeof(resultCosts) * nc));
@@ -394,6 +418,7 @@ bool session_finalize(mh_session* s, hipStream_t st) {
     MH_TRY_HIP(hipSetDevice(s->device));
     mh::LaunchArgs a = s->args();
     a.lay = s->geo.lay_ol;
+    if (s->track != mh::TRACK_OFF) a.st = s->d_best;  // report each chain's best configuration
     MH_TRY_HIP(mh::launch(mh::OP_FINAL, a, s->geo.L, s->geo.npl, s->geo.waves_ol, st));
     return true;
 }
@@ -410,8 +435,9 @@ bool session_download(mh_session* s, point* pts, resultCosts* costs) {
 }
 
 mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
-                           uint64_t seed) {
+                           uint64_t seed, int track) {
     mh_session* s = new mh_session();
+    s->track = track;
     s->device = device;
     s->room = room;
     s->n_chains = n_chains;
@@ -464,7 +490,8 @@ struct Shard {
 
 result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, positionAndRotation* cfg,
                      rectangle* clearances, rectangle* offlimits, vertex* vertices,
-                     vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg, uint64_t seed) {
+                     vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg, uint64_t seed,
+                     int track) {
     if (!gpuCfg) { set_error("gpuCfg is NULL"); return nullptr; }
     if (gpuCfg->gridxDim < 1) { set_error("gpuConfig.gridxDim must be >= 1"); return nullptr; }
     if (gpuCfg->iterations < 0) { set_error("gpuConfig.iterations must be >= 0"); return nullptr; }
@@ -498,7 +525,7 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         shards[k].count = chains * (int64_t)(k + 1) / (int64_t)devs.size() - shards[k].begin;
     }
     auto work = [&](Shard& sh) {
-        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed);
+        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed, track);
         if (!s) {
             sh.err = g_last_error;
             return;
@@ -541,7 +568,7 @@ MH_API result* KernelWrapper(relationshipStruct* rss, relationshipAngleStruct* r
                              vertex* vertices, vertex* surfaceRectangle, Surface* srf,
                              gpuConfig* gpuCfg) {
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, seed_from_env());
+                        gpuCfg, seed_from_env(), mh::TRACK_OFF);
 }
 
 MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStruct* rsa,
@@ -549,7 +576,19 @@ MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStr
                                    rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
                                    Surface* srf, gpuConfig* gpuCfg, uint64_t seed) {
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, seed);
+                        gpuCfg, seed, mh::TRACK_OFF);
+}
+
+MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct* rsa,
+                               positionAndRotation* cfg, rectangle* clearances,
+                               rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
+                               Surface* srf, gpuConfig* gpuCfg, const mh_options* opts) {
+    if (!opts)
+        return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle,
+                            srf, gpuCfg, seed_from_env(), mh::TRACK_OFF);
+    if (!check_options(opts)) return nullptr;
+    return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
+                        gpuCfg, opts->seed, opts->track_best);
 }
 
 MH_API void KernelFreeResult(result* res) {
@@ -586,7 +625,7 @@ MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationship
     }
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) { set_error("no HIP device available"); return -1; }
-    mh_session* s = session_create(room, device, 0, 0, 0);  // tables only
+    mh_session* s = session_create(room, device, 0, 0, 0, mh::TRACK_OFF);  // tables only
     if (!s) return -1;
     bool ok = true;
     double* d_cfgs = nullptr;
@@ -632,7 +671,28 @@ MH_API mh_session* mh_session_create(const relationshipStruct* rss,
         set_error("invalid HIP device " + std::to_string(device));
         return nullptr;
     }
-    return session_create(room, device, n_chains, chain_offset, seed);
+    return session_create(room, device, n_chains, chain_offset, seed, mh::TRACK_OFF);
+}
+
+MH_API mh_session* mh_session_create_ex(const relationshipStruct* rss,
+                                        const relationshipAngleStruct* rsa,
+                                        const positionAndRotation* cfg,
+                                        const rectangle* clearances, const rectangle* offlimits,
+                                        const vertex* vertices, const vertex* surfaceRectangle,
+                                        const Surface* srf, int device, int64_t n_chains,
+                                        int64_t chain_offset, const mh_options* opts) {
+    if (!opts) { set_error("opts is NULL"); return nullptr; }
+    if (!check_options(opts)) return nullptr;
+    if (n_chains < 0 || chain_offset < 0) { set_error("negative chain count or offset"); return nullptr; }
+    Room room;
+    if (!build_room(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf, room))
+        return nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) {
+        set_error("invalid HIP device " + std::to_string(device));
+        return nullptr;
+    }
+    return session_create(room, device, n_chains, chain_offset, opts->seed, opts->track_best);
 }
 
 MH_API int mh_session_run(mh_session* s, int iterations, void* stream) {

@@ -914,7 +914,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             m.bm_has = 0;
             m.bm_val = 0.0f;
             for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
-            m.pad[0] = m.pad[1] = 0;
+            m.best_total = cur[0];  // cfgBest := the initial configuration, Kernel.cu:779-782
+            m.pad = 0;
             a.meta[chain] = m;
         }
     } else if constexpr (OP == OP_STEP) {
@@ -928,6 +929,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         rng.bm_has = m0.bm_has;
         rng.bm_val = m0.bm_val;
         uint64_t accepted = m0.accepted;
+        float best_total = m0.best_total;
+        double* best_dst = a.best + chain * (int64_t)(F_COUNT * n);
         eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
 #if MH_STAMPS
         if (writer)
@@ -944,6 +947,11 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             SymRows<NPL> ss;
             eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y);
             MH_STAMP(ts);
+            // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
+            if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
+                best_total = sc[0];
+                save_best(ch, best_dst, n, r, L);
+            }
             if (accept(rng, sc[0], cur_total)) {
                 cur_total = sc[0];
                 sym = ss;
@@ -969,7 +977,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             m.bm_has = rng.bm_has;
             m.bm_val = rng.bm_val;
             for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
-            m.pad[0] = m.pad[1] = 0;
+            m.best_total = best_total;
+            m.pad = 0;
             a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
@@ -1006,6 +1015,13 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             dst[F_X * n + i] = ch.X[i];
             dst[F_Y * n + i] = ch.Y[i];
             dst[F_RY * n + i] = ch.RY[i];
+        }
+    }
+    if constexpr (OP == OP_INIT) {
+        if (a.track != TRACK_OFF) {  // cfgBest := cfgCurrent, Kernel.cu:779-782
+            if (r == 0) ch.aux->swap_a = -1;
+            wave_sync();
+            save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
         }
     }
 }

@@ -742,6 +742,8 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     rng.bm_has = m0.bm_has;
     rng.bm_val = m0.bm_val;
     uint64_t accepted = m0.accepted;
+    float best_total = m0.best_total;
+    double* best_dst = a.best + cidx * (int64_t)(F_COUNT * n);
     int rc = 0;  // which RM buffer holds the current rows
 #if MH_STAMPS
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last;
@@ -798,6 +800,11 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         float sc[8];
         replay<L>(ch, n, nxt.nmx, cnt_cl, cnt_sa, r, gbase, sc);
         DSTAMP(5);
+        // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
+        if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
+            best_total = sc[0];
+            if (live) save_best(ch, best_dst, n, r, L);
+        }
         if (accept(rng, sc[0], cur_total)) {
             cur_total = sc[0];
             ++accepted;
@@ -837,7 +844,8 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         m.bm_has = rng.bm_has;
         m.bm_val = rng.bm_val;
         for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
-        m.pad[0] = m.pad[1] = 0;
+        m.best_total = best_total;
+        m.pad = 0;
         a.meta[chain] = m;
     }
     if (live) {

@@ -77,13 +77,54 @@ struct ChainMeta {
     int bm_has;         // Box-Muller cache flag
     float bm_val;       // cached second normal
     float costs[8];     // resultCosts of the current state
-    int pad[2];
+    float best_total;   // best-of-chain tracking: totalCosts of the saved best configuration
+    int pad;
 };
 static_assert(sizeof(ChainMeta) == 64, "ChainMeta");
 
 // Pose layout in HBM: chain-major, six SoA rows of N doubles.
 // x, y, rotY enter the costs; z, rotX, rotZ (contiguous, F_Z..F_RZ) never do.
 enum { F_X = 0, F_Y = 1, F_RY = 2, F_Z = 3, F_RX = 4, F_RZ = 5, F_COUNT = 6 };
+
+// Best-of-chain tracking (the reference's commented-out cfgBest/bestCosts, Kernel.cu:779-782,
+// 808-816, 835-860): 0 off (the reference as shipped: output = final current state),
+// 1 = lowest totalCosts (the commented code's `starCosts->totalCosts < bestCosts->totalCosts`),
+// 2 = highest totalCosts (the direction Accept climbs, Kernel.cu:706-713).
+enum { TRACK_OFF = 0, TRACK_LOWEST = 1, TRACK_HIGHEST = 2 };
+
+__device__ __forceinline__ bool best_improves(int track, float star, float best) {
+    return track == TRACK_LOWEST ? star < best : star > best;  // NaN never improves
+}
+
+// Saves the proposed configuration (cfgStar, Kernel.cu:810-811) of one chain to its best
+// slot `dst` ([6][N] like the chain state). Lane r of the chain's L lanes writes objects
+// r, r+L, ... x, y, rotY come from LDS; z, rotX, rotZ live in HBM (`ch.zrr`) and are swapped
+// there only on accept, so a pending swap (aux->swap_a/b >= 0) is applied here as
+// commit_swap_zrr would: ka takes kb's values, kb takes ka's rounded to float.
+template <class Ptrs>
+__device__ __forceinline__ void save_best(const Ptrs& ch, double* dst, int n, int r, int L) {
+    const int ka = ch.aux->swap_a, kb = ch.aux->swap_b;
+    for (int i = r; i < n; i += L) {
+        dst[F_X * n + i] = ch.X[i];
+        dst[F_Y * n + i] = ch.Y[i];
+        dst[F_RY * n + i] = ch.RY[i];
+        int src = i;
+        bool rnd = false;
+        if (ka >= 0) {
+            if (i == kb) {
+                src = ka;
+                rnd = true;
+            } else if (i == ka) {
+                src = kb;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const double v = ch.zrr[f * n + src];
+            dst[(F_Z + f) * n + i] = rnd ? (double)(float)v : v;
+        }
+    }
+}
 
 // Per-chain scalars of the full-evaluation kernel (mh_chain.hip ChainAux), bytes.
 #if defined(MH_STAMPS) && MH_STAMPS

@@ -27,6 +27,8 @@ struct LaunchArgs {
     int64_t chain_offset;    // global id of local chain 0 (Philox subsequence)
     uint64_t seed;
     int iterations;
+    int track;               // TRACK_OFF / TRACK_LOWEST / TRACK_HIGHEST
+    double* best;            // [n_chains][6][N] best-of-chain configurations (track != 0)
     ChainLds lay;
     DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
 };

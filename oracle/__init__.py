@@ -67,6 +67,9 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_run_chains.restype = C.c_int
     lib.orc_run_chains_state.argtypes = lib.orc_run_chains.argtypes
     lib.orc_run_chains_state.restype = C.c_int
+    lib.orc_run_chains_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                      C.c_int, C.c_int, C.c_void_p, C.c_void_p, P(C.c_int64)]
+    lib.orc_run_chains_ex.restype = C.c_int
     lib.orc_rand_int.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.orc_rand_int.restype = C.c_int
     lib.orc_pick_object.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
@@ -108,16 +111,28 @@ def costs(room, cfg=None) -> np.ndarray:
     return np.frombuffer(bytes(out), dtype=np.float32).copy()
 
 
+class OrcOptions(C.Structure):  # mh_options, include/mh_kernel.h
+    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
 def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int = 0,
-               threads: int = 1, state: bool = False):
+               threads: int = 1, state: bool = False, track: int = 0):
     """Runs the restated chain loop. Returns (points [chains,N,6] float32 or state
-    [chains,N,9] float64 (x,y,z,rotX,rotY,rotZ,frozen,length,width), costs [chains,8] float32,
-    accepted [chains] int64)."""
+    [chains,N,6] float64 (x,y,z,rotX,rotY,rotZ), costs [chains,8] float32, accepted [chains]
+    int64). `track` = 1 / 2 returns each chain's lowest / highest-total configuration instead
+    of its final one (the reference's commented-out cfgBest, Kernel.cu:779-816)."""
     lib = load()
     n = room.n
     cs = (C.c_float * (8 * chains))()
     acc = (C.c_int64 * chains)()
-    if state:
+    if track:
+        state = True
+        buf = (C.c_uint8 * (72 * n * chains))()
+        opts = OrcOptions(seed, track)
+        rc = lib.orc_run_chains_ex(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p),
+                                   C.byref(opts), chain_begin, chains, iterations, threads,
+                                   C.cast(buf, C.c_void_p), C.cast(cs, C.c_void_p), acc)
+    elif state:
         from numpy.lib import recfunctions  # noqa: F401
         buf = (C.c_uint8 * (72 * n * chains))()
         rc = lib.orc_run_chains_state(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p), seed,

@@ -526,6 +526,7 @@ typedef struct {
     int64_t chain_begin;
     int64_t lo, hi; /* local chain range for this worker */
     int iterations;
+    int track; /* MH_TRACK_* */
     point* out_points;
     positionAndRotation* out_state;
     resultCosts* out_costs;
@@ -533,23 +534,36 @@ typedef struct {
 } chain_job;
 
 static void run_one(const chain_job* job, int64_t local, positionAndRotation* cur,
-                    positionAndRotation* star) {
+                    positionAndRotation* star, positionAndRotation* best) {
     const int n = job->room->srf->nObjs;
     orc_rng r;
     orc_rng_init(&r, job->seed, (uint64_t)(job->chain_begin + local));
     memcpy(cur, job->cfg, sizeof(positionAndRotation) * n);
     resultCosts cc, sc;
     orc_costs(job->room, cur, &cc);
+    /* Best-of-chain, the reference's commented-out intent: cfgBest := cfgCurrent
+     * (Kernel.cu:779-782); star replaces best when it improves, before Accept (:808-816). */
+    resultCosts bc = cc;
+    if (job->track) memcpy(best, cur, sizeof(positionAndRotation) * n);
     int64_t acc = 0;
     for (int it = 0; it < job->iterations; ++it) {
         memcpy(star, cur, sizeof(positionAndRotation) * n);
         orc_propose(job->room, star, &r);
         orc_costs(job->room, star, &sc);
+        if (job->track && (job->track == MH_TRACK_LOWEST ? sc.totalCosts < bc.totalCosts
+                                                         : sc.totalCosts > bc.totalCosts)) {
+            memcpy(best, star, sizeof(positionAndRotation) * n);
+            bc = sc;
+        }
         if (orc_accept(sc.totalCosts, cc.totalCosts, &r)) {
             memcpy(cur, star, sizeof(positionAndRotation) * n);
             cc = sc;
             ++acc;
         }
+    }
+    if (job->track) { /* the output is cfgBest / bestCosts (Kernel.cu:840-860, commented out) */
+        memcpy(cur, best, sizeof(positionAndRotation) * n);
+        cc = bc;
     }
     if (job->out_points) {
         point* p = job->out_points + local * n;
@@ -569,18 +583,22 @@ static void* chain_worker(void* arg) {
     const int n = job->room->srf->nObjs;
     positionAndRotation* cur = malloc(sizeof(positionAndRotation) * n);
     positionAndRotation* star = malloc(sizeof(positionAndRotation) * n);
-    for (int64_t c = job->lo; c < job->hi; ++c) run_one(job, c, cur, star);
+    positionAndRotation* best = malloc(sizeof(positionAndRotation) * n);
+    for (int64_t c = job->lo; c < job->hi; ++c) run_one(job, c, cur, star, best);
     free(cur);
     free(star);
+    free(best);
     return NULL;
 }
 
 static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
-                      int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
+                      int track, int64_t chain_begin, int64_t n_chains, int iterations,
+                      int nthreads,
                       point* out_points, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted) {
     if (orc_validate(room, cfg) != 0) return -1;
     if (n_chains < 0 || iterations < 0) return fail("negative chain or step count%ld", 0);
+    if (track < MH_TRACK_OFF || track > MH_TRACK_HIGHEST) return fail("bad track_best %ld", track);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > n_chains) nthreads = (int)(n_chains > 0 ? n_chains : 1);
     chain_job* jobs = calloc((size_t)nthreads, sizeof(chain_job));
@@ -588,7 +606,7 @@ static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint
     for (int t = 0; t < nthreads; ++t) {
         chain_job j = {room, cfg, seed, chain_begin,
                        n_chains * t / nthreads, n_chains * (t + 1) / nthreads,
-                       iterations, out_points, out_state, out_costs, out_accepted};
+                       iterations, track, out_points, out_state, out_costs, out_accepted};
         jobs[t] = j;
     }
     for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, chain_worker, &jobs[t]);
@@ -602,14 +620,22 @@ static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint
 int orc_run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                    int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                    point* out_points, resultCosts* out_costs, int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, chain_begin, n_chains, iterations, nthreads, out_points,
-                      NULL, out_costs, out_accepted);
+    return run_chains(room, cfg, seed, MH_TRACK_OFF, chain_begin, n_chains, iterations, nthreads,
+                      out_points, NULL, out_costs, out_accepted);
 }
 
 int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                          int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                          positionAndRotation* out_state, resultCosts* out_costs,
                          int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, chain_begin, n_chains, iterations, nthreads, NULL,
-                      out_state, out_costs, out_accepted);
+    return run_chains(room, cfg, seed, MH_TRACK_OFF, chain_begin, n_chains, iterations, nthreads,
+                      NULL, out_state, out_costs, out_accepted);
+}
+
+int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
+                      const mh_options* opts, int64_t chain_begin, int64_t n_chains,
+                      int iterations, int nthreads, positionAndRotation* out_state,
+                      resultCosts* out_costs, int64_t* out_accepted) {
+    return run_chains(room, cfg, opts->seed, opts->track_best, chain_begin, n_chains, iterations,
+                      nthreads, NULL, out_state, out_costs, out_accepted);
 }

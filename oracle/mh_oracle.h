@@ -95,6 +95,14 @@ int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, u
                          positionAndRotation* out_state, resultCosts* out_costs,
                          int64_t* out_accepted);
 
+/* orc_run_chains_state with the options of KernelWrapperEx (include/mh_kernel.h): seed and
+ * best-of-chain tracking. With tracking on, out_state / out_costs hold each chain's best
+ * configuration and its costs. */
+int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
+                      const mh_options* opts, int64_t chain_begin, int64_t n_chains,
+                      int iterations, int nthreads, positionAndRotation* out_state,
+                      resultCosts* out_costs, int64_t* out_accepted);
+
 #ifdef __cplusplus
 }
 #endif

@@ -318,3 +318,93 @@ def test_group_collectives(mh, hiplib, L):
             assert np.array_equal(got["scan"][sl], np.concatenate([[0], np.cumsum(ig)[:-1]]))
             assert np.all(got["total"][sl] == ig.sum())
             assert np.all(got["imax"][sl] == ig.max()) and np.all(got["isum"][sl] == ig.sum())
+
+
+@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("track", [1, 2])
+@pytest.mark.parametrize("kind,n,chains,steps", [
+    ("main", 32, 96, 300),
+    ("frozen", 16, 128, 400),
+    ("syn", 9, 128, 400),
+    ("syn", 64, 48, 1200),   # two launches: the best total is carried in the chain meta
+    ("syn", 2, 64, 200),
+])
+def test_best_of_chain_matches_oracle(mh, orc, hiplib, monkeypatch, step, track, kind, n, chains,
+                                      steps):
+    """Best-of-chain tracking (KernelWrapperEx / mh_session_create_ex; the reference's
+    commented-out cfgBest, Kernel.cu:779-782,808-816,840-860) against the oracle's restatement:
+    the best configuration and its eight costs, bit for bit, for both step kernels."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    room = _room(mh, kind, n)
+    seed = 9100 + n + track
+    with mh.Session(room, chains, seed=seed, track=track) as s:
+        assert s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_state, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8, track=track)
+    ref_pts = ref_state.astype(np.float32)
+    same = np.all(pts.view(np.uint32) == ref_pts.view(np.uint32), axis=(1, 2)) & np.all(
+        costs.view(np.uint32) == ref_costs.view(np.uint32), axis=1)
+    print(f"best({track}) {step} {kind} N={n}: {same.mean() * 100:.2f}% of chains bit-identical")
+    assert same.mean() >= 0.99
+    # the best is at least as good as the final current state of the same trajectory
+    _, cur_costs = mh.kernel_wrapper(room, chains, steps, seed=seed)
+    if track == 1:
+        assert np.all(costs[:, 0] <= cur_costs[:, 0])
+    else:
+        assert np.all(costs[:, 0] >= cur_costs[:, 0])
+
+
+def test_best_of_chain_kernel_wrapper_ex(mh, orc, hiplib):
+    """KernelWrapperEx returns the best configurations in the reference's result layout, and
+    track_best = OFF through it equals KernelWrapperSeeded."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed = 256, 500, 77
+    p_best, c_best = mh.kernel_wrapper(room, chains, steps, seed=seed, track=2)
+    ref_state, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8, track=2)
+    assert np.array_equal(p_best.view(np.uint32), ref_state.astype(np.float32).view(np.uint32))
+    assert np.array_equal(c_best.view(np.uint32), ref_costs.view(np.uint32))
+    p0, c0 = mh.kernel_wrapper(room, chains, steps, seed=seed)
+    lib = mh.load_library()
+    g = mh.abi.gpuConfig(chains, 0, 64, 0, 0, steps)
+    res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh.abi.mh_options(seed, 0)))
+    assert res
+    try:
+        pts = (mh.abi.point * (chains * room.n)).from_address(C.cast(res[0].points, C.c_void_p).value)
+        p1 = np.frombuffer(bytes(memoryview(pts)), dtype=np.float32).reshape(chains, room.n, 6)
+    finally:
+        lib.KernelFreeResult(res)
+    assert np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
+
+
+def test_best_of_chain_full_size(mh, hiplib):
+    """Config 3's shape (65,536 chains, N = 64) with tracking on: the reported best costs equal
+    a fresh evaluation of the reported best configurations (sampled), and best >= final."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed = 65536, 300, 4242
+    with mh.Session(room, chains, seed=seed, track=2) as s:
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+        summ = s.summary()
+    with mh.Session(room, chains, seed=seed) as s0:
+        s0.run(steps)
+        s0.finalize()
+        _, cur = s0.download()
+    assert np.all(costs[:, 0] >= cur[:, 0])
+    assert summ.best_total == costs[:, 0].max()
+    idx = np.random.default_rng(0).choice(chains, 64, replace=False)
+    cfgs = (mh.abi.positionAndRotation * (len(idx) * room.n))()
+    base = np.ctypeslib.as_array(room.cfg)
+    for j, c in enumerate(idx):
+        for i in range(room.n):
+            p = pts[c, i]
+            cfgs[j * room.n + i] = mh.abi.positionAndRotation(
+                *map(float, p), bool(base[i]["frozen"]), float(base[i]["length"]),
+                float(base[i]["width"]))
+    # the float points are a rounding of the double state, so compare totals loosely here;
+    # the bit-exact check is test_best_of_chain_matches_oracle
+    fresh = mh.evaluate_costs(room, cfgs)
+    rel = np.abs(fresh[:, 0] - costs[idx, 0]) / np.maximum(np.abs(costs[idx, 0]), 1)
+    assert np.median(rel) < 1e-3

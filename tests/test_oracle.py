@@ -257,3 +257,60 @@ def test_accept_rule(orc):
     assert lib.orc_accept(10.0 - 0.5 * math.log(2) - 1e-3, 10.0, C.byref(r)) == 0
     r = _rng_with_words(orc, [0xFFFFFFFF] * 4)                    # u = 1.0f: never accepts
     assert lib.orc_accept(1e6, 0.0, C.byref(r)) == 0
+
+
+def _copy(arr):
+    out = (arr._type_ * len(arr))()
+    C.memmove(out, arr, C.sizeof(out))
+    return out
+
+
+@pytest.mark.parametrize("track", [1, 2])
+def test_best_of_chain_restatement(mh, orc, track):
+    """orc_run_chains_ex's best-of-chain tracking against the reference's commented-out loop
+    (Kernel.cu:779-782, 808-816), re-walked step by step here through orc_propose / orc_costs /
+    orc_accept: best starts as the initial configuration, every star is compared before Accept
+    with a strict comparison, and the output is cfgBest with bestCosts."""
+    lib = orc.load()
+    room = mh.synthetic_room(8)
+    n, steps, seed, chains = room.n, 120, 31337, 3
+    ref_state, ref_costs, _ = orc.run_chains(room, chains, steps, seed, track=track)
+    better = (lambda s, b: s < b) if track == 1 else (lambda s, b: s > b)
+    orm = orc.orc_room(room)
+    for c in range(chains):
+        rng = orc.OrcRng()
+        lib.orc_rng_init(C.byref(rng), seed, c)
+        cur = mh.clone_cfg(room)
+        cc = orc.costs(room, cur)
+        best, bc = _copy(cur), cc.copy()
+        for _ in range(steps):
+            star = _copy(cur)
+            lib.orc_propose(C.byref(orm), C.cast(star, C.c_void_p), C.byref(rng))
+            sc = orc.costs(room, star)
+            if better(sc[0], bc[0]):
+                best, bc = _copy(star), sc
+            if lib.orc_accept(float(sc[0]), float(cc[0]), C.byref(rng)):
+                cur, cc = star, sc
+        got = np.array([[b.x, b.y, b.z, b.rotX, b.rotY, b.rotZ] for b in best])
+        assert np.array_equal(got, ref_state[c])
+        assert np.array_equal(bc.view(np.uint32), ref_costs[c].view(np.uint32))
+
+
+def test_best_of_chain_bounds(mh, orc):
+    """Lowest <= initial and final; highest >= initial and final; the reported costs are the
+    costs of the reported configuration."""
+    room = mh.synthetic_room(16)
+    chains, steps, seed = 16, 400, 5
+    init = orc.costs(room)[0]
+    _, fin, _ = orc.run_chains(room, chains, steps, seed, threads=4)
+    lo_s, lo, _ = orc.run_chains(room, chains, steps, seed, threads=4, track=1)
+    hi_s, hi, _ = orc.run_chains(room, chains, steps, seed, threads=4, track=2)
+    assert np.all(lo[:, 0] <= init) and np.all(lo[:, 0] <= fin[:, 0])
+    assert np.all(hi[:, 0] >= init) and np.all(hi[:, 0] >= fin[:, 0])
+    base = np.ctypeslib.as_array(room.cfg)
+    for c in (0, chains - 1):
+        cfg = mh.clone_cfg(room)
+        for i in range(room.n):
+            cfg[i].x, cfg[i].y, cfg[i].z, cfg[i].rotX, cfg[i].rotY, cfg[i].rotZ = hi_s[c, i]
+            assert cfg[i].frozen == base[i]["frozen"]
+        assert np.array_equal(orc.costs(room, cfg).view(np.uint32), hi[c].view(np.uint32))
