@@ -157,12 +157,20 @@ typedef enum mh_track_best {
     MH_TRACK_HIGHEST = 2  /* the same with `>`: the direction Accept climbs (Kernel.cu:706-713) */
 } mh_track_best;
 
+typedef enum mh_rng_kind {
+    MH_RNG_PHILOX = 0,        /* rocRAND Philox4x32-10, key = seed, chain c = subsequence c */
+    MH_RNG_CURAND_XORWOW = 1  /* cuRAND's XORWOW as the reference seeds it: chain c runs
+                                 curand_init((unsigned)(seed + c), c, 0) (Kernel.cu:151-159,943)
+                                 and draws curand_uniform / curand_normal (Kernel.cu:569-710) */
+} mh_rng_kind;
+
 typedef struct mh_options {
-    uint64_t seed;       /* Philox4x32-10 key; chain c draws subsequence c */
+    uint64_t seed;       /* RNG seed (see mh_rng_kind) */
     int32_t track_best;  /* mh_track_best. The initial configuration is the first best; every
                             proposal (accepted or not) is compared before the accept test; ties
                             keep the earlier one. */
-    int32_t reserved[5]; /* must be zero */
+    int32_t rng;         /* mh_rng_kind */
+    int32_t reserved[4]; /* must be zero */
 } mh_options;
 
 /* KernelWrapper with options (NULL = KernelWrapper's defaults with seed $MH_SEED/time). With
@@ -261,6 +269,11 @@ MH_API int mh_debug_collectives(int L, const float* v, const int* iv, int* out);
 
 MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
                         float* out_uniform, float* out_normal);
+
+/* mh_debug_rng for either stream (mh_rng_kind). For MH_RNG_CURAND_XORWOW the stream is
+ * curand_init(seed, subsequence, 0) as given (the chains add their id to the seed). */
+MH_API int mh_debug_rng_ex(int rng, uint64_t seed, uint64_t subsequence, int n,
+                           unsigned int* out_u32, float* out_uniform, float* out_normal);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -85,10 +85,12 @@ class mh_summary(C.Structure):
 
 
 class mh_options(C.Structure):
-    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("reserved", C.c_int32 * 5)]
+    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("rng", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 MH_TRACK_OFF, MH_TRACK_LOWEST, MH_TRACK_HIGHEST = 0, 1, 2
+MH_RNG_PHILOX, MH_RNG_CURAND_XORWOW = 0, 1
 
 STRUCT_LAYOUT = {  # (size, {field: offset}) as static_assert-ed in include/mh_kernel.h
     vertex: (24, {}),
@@ -104,7 +106,7 @@ STRUCT_LAYOUT = {  # (size, {field: offset}) as static_assert-ed in include/mh_k
     resultCosts: (32, {}),
     result: (40, {"costs": 8}),
     mh_summary: (40, {}),
-    mh_options: (32, {"track_best": 8}),
+    mh_options: (32, {"track_best": 8, "rng": 12}),
 }
 
 COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointCosts",
@@ -115,7 +117,7 @@ EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelWrapperEx", "KernelFre
            "KernelLastError", "KernelEvaluateCosts", "mh_session_create", "mh_session_create_ex",
            "mh_session_run", "mh_session_finalize",
            "mh_session_download", "mh_session_current_costs", "mh_session_summary", "mh_session_geometry",
-           "mh_session_destroy", "mh_debug_rng", "mh_debug_collectives"]
+           "mh_session_destroy", "mh_debug_rng", "mh_debug_rng_ex", "mh_debug_collectives"]
 
 P = C.POINTER
 
@@ -176,6 +178,9 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_debug_rng.argtypes = [C.c_uint64, C.c_uint64, C.c_int, P(C.c_uint32), P(C.c_float),
                                  P(C.c_float)]
     lib.mh_debug_rng.restype = C.c_int
+    lib.mh_debug_rng_ex.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, P(C.c_uint32),
+                                    P(C.c_float), P(C.c_float)]
+    lib.mh_debug_rng_ex.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -232,16 +237,16 @@ def points_to_array(pts, count: int) -> np.ndarray:
 # ---- calls -----------------------------------------------------------------------------------
 
 def kernel_wrapper(room: Room, chains: int, iterations: int, seed: int | None = None,
-                   block_x: int = 64, track: int = MH_TRACK_OFF):
-    """Calls KernelWrapper (or KernelWrapperSeeded, or KernelWrapperEx when `track` is set)
-    exactly as the reference's caller does and returns (points [chains, N, 6] float32,
+                   block_x: int = 64, track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX):
+    """Calls KernelWrapper (or KernelWrapperSeeded, or KernelWrapperEx when `track` or `rng`
+    is set) exactly as the reference's caller does and returns (points [chains, N, 6] float32,
     costs [chains, 8] float32)."""
     lib = load_library()
     g = gpuConfig(chains, 0, block_x, 0, 0, iterations)
-    if track:
+    if track or rng:
         if seed is None:
-            raise ValueError("best-of-chain tracking needs an explicit seed")
-        res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh_options(seed, track)))
+            raise ValueError("KernelWrapperEx needs an explicit seed")
+        res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh_options(seed, track, rng)))
     elif seed is None:
         res = lib.KernelWrapper(*room.args(), C.byref(g))
     else:
@@ -276,12 +281,12 @@ def evaluate_costs(room: Room, cfgs) -> np.ndarray:
     return costs_to_array(out)[:k]
 
 
-def debug_rng(seed: int, subsequence: int, n: int):
+def debug_rng(seed: int, subsequence: int, n: int, rng: int = MH_RNG_PHILOX):
     lib = load_library()
     u = (C.c_uint32 * n)()
     f = (C.c_float * n)()
     g = (C.c_float * n)()
-    if lib.mh_debug_rng(C.c_uint64(seed), C.c_uint64(subsequence), n, u, f, g) != 0:
+    if lib.mh_debug_rng_ex(rng, C.c_uint64(seed), C.c_uint64(subsequence), n, u, f, g) != 0:
         raise MHError(last_error(lib))
     return (np.frombuffer(bytes(u), dtype=np.uint32).copy(),
             np.frombuffer(bytes(f), dtype=np.float32).copy(),
@@ -307,14 +312,14 @@ class Session:
     """Device-resident chains: the shard one rank owns (chain ids [offset, offset + chains))."""
 
     def __init__(self, room: Room, chains: int, seed: int, device: int = 0, chain_offset: int = 0,
-                 track: int = MH_TRACK_OFF):
+                 track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX):
         self.lib = load_library()
         self.room = room
         self.chains = chains
         self.chain_offset = chain_offset
-        if track:
+        if track or rng:
             h = self.lib.mh_session_create_ex(*room.args(), device, chains, chain_offset,
-                                              C.byref(mh_options(seed, track)))
+                                              C.byref(mh_options(seed, track, rng)))
         else:
             h = self.lib.mh_session_create(*room.args(), device, chains, chain_offset,
                                            C.c_uint64(seed))

@@ -23,6 +23,8 @@
 
 #include "mh_launch.h"
 
+static_assert((int)mh::RNG_PHILOX == MH_RNG_PHILOX &&
+                  (int)mh::RNG_CURAND_XORWOW == MH_RNG_CURAND_XORWOW, "RNG kinds");
 static_assert((int)mh::TRACK_OFF == MH_TRACK_OFF && (int)mh::TRACK_LOWEST == MH_TRACK_LOWEST &&
                   (int)mh::TRACK_HIGHEST == MH_TRACK_HIGHEST,
               "device and ABI best-tracking modes");
@@ -282,7 +284,11 @@ bool check_options(const mh_options* o) {
         set_error("mh_options.track_best must be MH_TRACK_OFF, MH_TRACK_LOWEST or MH_TRACK_HIGHEST");
         return false;
     }
-    for (int k = 0; k < 5; ++k)
+    if (o->rng < MH_RNG_PHILOX || o->rng > MH_RNG_CURAND_XORWOW) {
+        set_error("mh_options.rng must be MH_RNG_PHILOX or MH_RNG_CURAND_XORWOW");
+        return false;
+    }
+    for (int k = 0; k < 4; ++k)
         if (o->reserved[k] != 0) {
             set_error("mh_options.reserved must be zero");
             return false;
@@ -306,6 +312,8 @@ struct mh_session {
     int64_t n_chains = 0, chain_offset = 0;
     uint64_t seed = 0;
     int track = mh::TRACK_OFF;
+    int rng = mh::RNG_PHILOX;
+    unsigned int* d_xw = nullptr;  // [n_chains][6] XORWOW states (rng == RNG_CURAND_XORWOW)
     mh::ObjConst* d_obj = nullptr;
     mh::ClrConst* d_clr = nullptr;
     mh::RelConst* d_rel = nullptr;
@@ -334,6 +342,8 @@ struct mh_session {
         a.iterations = 0;
         a.track = track;
         a.best = d_best;
+        a.rng = rng;
+        a.xw = d_xw;
         a.lay = geo.lay;
         a.dlay = geo.dlay;
         return a;
@@ -354,6 +364,7 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_cfg0);
     (void)hipFree(s->d_st);
     (void)hipFree(s->d_best);
+    (void)hipFree(s->d_xw);
     (void)hipFree(s->d_meta);
     (void)hipFree(s->d_pts);
     (void)hipFree(s->d_costs);
@@ -383,6 +394,10 @@ bool session_init(mh_session* s) {
     MH_TRY_HIP(hipMalloc((void**)&s->d_st, sizeof(double) * mh::F_COUNT * n * nc));
     if (s->track != mh::TRACK_OFF)
         MH_TRY_HIP(hipMalloc((void**)&s->d_best, sizeof(double) * mh::F_COUNT * n * nc));
+    if (s->rng == mh::RNG_CURAND_XORWOW) {
+        MH_TRY_HIP(hipMalloc((void**)&s->d_xw, sizeof(unsigned int) * 6 * nc));
+        MH_TRY_HIP(mh::launch_xorwow_init(s->seed, s->chain_offset, s->n_chains, s->d_xw, s->stream));
+    }
     MH_TRY_HIP(hipMalloc((void**)&s->d_meta, sizeof(mh::ChainMeta) * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_pts, sizeof(point) * n * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_costs, sizeof(resultCosts) * nc));
@@ -435,9 +450,10 @@ bool session_download(mh_session* s, point* pts, resultCosts* costs) {
 }
 
 mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
-                           uint64_t seed, int track) {
+                           uint64_t seed, int track, int rng = mh::RNG_PHILOX) {
     mh_session* s = new mh_session();
     s->track = track;
+    s->rng = rng;
     s->device = device;
     s->room = room;
     s->n_chains = n_chains;
@@ -491,7 +507,7 @@ struct Shard {
 result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, positionAndRotation* cfg,
                      rectangle* clearances, rectangle* offlimits, vertex* vertices,
                      vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg, uint64_t seed,
-                     int track) {
+                     int track, int rng = mh::RNG_PHILOX) {
     if (!gpuCfg) { set_error("gpuCfg is NULL"); return nullptr; }
     if (gpuCfg->gridxDim < 1) { set_error("gpuConfig.gridxDim must be >= 1"); return nullptr; }
     if (gpuCfg->iterations < 0) { set_error("gpuConfig.iterations must be >= 0"); return nullptr; }
@@ -525,7 +541,7 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         shards[k].count = chains * (int64_t)(k + 1) / (int64_t)devs.size() - shards[k].begin;
     }
     auto work = [&](Shard& sh) {
-        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed, track);
+        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed, track, rng);
         if (!s) {
             sh.err = g_last_error;
             return;
@@ -588,7 +604,7 @@ MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct*
                             srf, gpuCfg, seed_from_env(), mh::TRACK_OFF);
     if (!check_options(opts)) return nullptr;
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, opts->seed, opts->track_best);
+                        gpuCfg, opts->seed, opts->track_best, opts->rng);
 }
 
 MH_API void KernelFreeResult(result* res) {
@@ -692,7 +708,8 @@ MH_API mh_session* mh_session_create_ex(const relationshipStruct* rss,
         set_error("invalid HIP device " + std::to_string(device));
         return nullptr;
     }
-    return session_create(room, device, n_chains, chain_offset, opts->seed, opts->track_best);
+    return session_create(room, device, n_chains, chain_offset, opts->seed, opts->track_best,
+                          opts->rng);
 }
 
 MH_API int mh_session_run(mh_session* s, int iterations, void* stream) {
@@ -755,14 +772,23 @@ MH_API void mh_session_destroy(mh_session* s) { free_session(s); }
 // draws, exactly as the chain kernel draws them. Returns 0 on success.
 MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
                         float* out_uniform, float* out_normal) {
-    if (n < 0 || !out_u32 || !out_uniform || !out_normal) { set_error("bad arguments"); return -1; }
+    return mh_debug_rng_ex(MH_RNG_PHILOX, seed, subsequence, n, out_u32, out_uniform, out_normal);
+}
+
+MH_API int mh_debug_rng_ex(int rng, uint64_t seed, uint64_t subsequence, int n,
+                           unsigned int* out_u32, float* out_uniform, float* out_normal) {
+    if (n < 0 || !out_u32 || !out_uniform || !out_normal || rng < MH_RNG_PHILOX ||
+        rng > MH_RNG_CURAND_XORWOW) {
+        set_error("bad arguments");
+        return -1;
+    }
     if (n == 0) return 0;
     unsigned int* d_u = nullptr;
     float *d_f = nullptr, *d_n = nullptr;
     hipError_t e = hipMalloc((void**)&d_u, sizeof(unsigned int) * n);
     if (e == hipSuccess) e = hipMalloc((void**)&d_f, sizeof(float) * n);
     if (e == hipSuccess) e = hipMalloc((void**)&d_n, sizeof(float) * n);
-    if (e == hipSuccess) e = mh::launch_rng(seed, subsequence, n, d_u, d_f, d_n, nullptr);
+    if (e == hipSuccess) e = mh::launch_rng(rng, seed, subsequence, n, d_u, d_f, d_n, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out_u32, d_u, sizeof(unsigned int) * n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(out_uniform, d_f, sizeof(float) * n, hipMemcpyDeviceToHost);

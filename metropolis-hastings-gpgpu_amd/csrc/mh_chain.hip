@@ -21,6 +21,9 @@
 #include <stdlib.h>
 
 #include "mh_common.h"
+#ifndef MH_CHAIN_XW_TU
+#include <rocrand/rocrand_xorwow.h>
+#endif
 #ifndef MH_DOUBLE
 #define MH_DOUBLE 0  // cost-probe builds: run phase k twice when bit k is set; product = 0
                      // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay)
@@ -31,8 +34,10 @@
 #define MH_STAMPS 0  // diagnostic builds (tools/build_stamps.sh) time each phase; product = 0
 #endif
 
-#if MH_STAMPS
+#if MH_STAMPS && !defined(MH_CHAIN_XW_TU)
 __device__ unsigned long long g_phase_cycles[16];
+#elif MH_STAMPS
+extern __device__ unsigned long long g_phase_cycles[16];
 #define MH_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define MH_PHASE(ch, k, t0) do { unsigned long long _t; MH_STAMP(_t); (ch).aux->cyc[k] += _t - (t0); (t0) = _t; } while (0)
 #else
@@ -718,7 +723,8 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, 
 
 // Applies one proposal to the configuration in LDS; `writer` also records the overwritten
 // objects in ch.aux so a rejection can undo them. Returns the objects it changed (-1: none).
-__device__ int2 propose(ChainRng& rng, const DevRoom& rm, const unsigned char* frozen,
+template <class Rng>
+__device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen,
                         const ChainPtrs& ch, bool writer) {
     const int n = rm.n;
     const int mode = rand_int(rng, 2, 0);
@@ -818,6 +824,9 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
 template <int L, int NPL, int OP>
 __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // OP_STEP_XW: OP_STEP drawing from the cuRAND XORWOW stream instead of Philox.
+    constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_XW);
+    using Rng = typename RngOf<OP == OP_STEP_XW>::type;
     constexpr int G = 64 / L;
     const int n = a.rm.n;
     const int lane = threadIdx.x & 63;
@@ -918,16 +927,14 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             m.pad = 0;
             a.meta[chain] = m;
         }
-    } else if constexpr (OP == OP_STEP) {
+    } else if constexpr (STEP) {
         const ChainMeta m0 = a.meta[chain];
         const bool writer = (r == 0);
         if (writer)
             for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
         float cur_total = m0.costs[0];
-        ChainRng rng;
-        rng.init(a.seed, (uint64_t)(a.chain_offset + chain), m0.draws);
-        rng.bm_has = m0.bm_has;
-        rng.bm_val = m0.bm_val;
+        Rng rng;
+        rng_load(rng, a, chain, m0);
         uint64_t accepted = m0.accepted;
         float best_total = m0.best_total;
         double* best_dst = a.best + chain * (int64_t)(F_COUNT * n);
@@ -976,6 +983,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             m.accepted = accepted;
             m.bm_has = rng.bm_has;
             m.bm_val = rng.bm_val;
+            rng_save(rng, a, chain);
             for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
             m.best_total = best_total;
             m.pad = 0;
@@ -1009,7 +1017,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         }
     }
 
-    if constexpr (OP == OP_INIT || OP == OP_STEP) {
+    if constexpr (OP == OP_INIT || STEP) {
         double* dst = a.st + chain * (int64_t)(F_COUNT * n);
         for (int i = r; i < n; i += L) {
             dst[F_X * n + i] = ch.X[i];
@@ -1026,6 +1034,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     }
 }
 
+#ifndef MH_CHAIN_XW_TU
 // ---- summary reduction (for the multi-GPU best-cost all-gather) ---------------------------
 
 __global__ void __launch_bounds__(1024) mh_summary_kernel(const resultCosts* costs,
@@ -1093,6 +1102,68 @@ __global__ void mh_rng_kernel(uint64_t seed, uint64_t subsequence, int n, unsign
     for (int i = 0; i < n; ++i) uni[i] = r.uniform();
     r.init(seed, subsequence, 0);
     for (int i = 0; i < n; ++i) nrm[i] = r.normal();
+}
+
+// ---- cuRAND XORWOW seeding: curand_init(seed + id, id, 0) per chain (Kernel.cu:159) --------
+
+// rocRAND's xorwow_engine implements the same recurrence and the same 2^67-draw subsequence
+// jump (its precomputed jump matrices depend only on the recurrence); it differs from cuRAND in
+// the seed-scrambling constants alone. This engine applies cuRAND's constants
+// (_curand_init_scratch in curand_kernel.h) and then rocRAND's subsequence jump.
+struct CurandXorwowSeeder : rocrand_device::xorwow_engine {
+    __device__ CurandXorwowSeeder(unsigned long long seed, unsigned long long subsequence)
+        : rocrand_device::xorwow_engine(0ull, 0ull, 0ull) {
+        const unsigned int s0 = (unsigned int)seed ^ 0xaad26b49u;
+        const unsigned int s1 = (unsigned int)(seed >> 32) ^ 0xf7dcefddu;
+        const unsigned int t0 = 1099087573u * s0;
+        const unsigned int t1 = 2591861531u * s1;
+        m_state.d = 6615241u + t1 + t0;
+        m_state.x[0] = 123456789u + t0;
+        m_state.x[1] = 362436069u ^ t0;
+        m_state.x[2] = 521288629u + t1;
+        m_state.x[3] = 88675123u ^ t1;
+        m_state.x[4] = 5783321u + t0;
+        discard_subsequence(subsequence);
+    }
+    __device__ void store(unsigned int* w) const {
+        w[0] = m_state.d;
+        for (int k = 0; k < 5; ++k) w[1 + k] = m_state.x[k];
+    }
+};
+
+// Chain c (global id g = chain_offset + c) gets curand_init((unsigned)(seed + g), g, 0): the
+// reference adds the thread id to an unsigned int seed (Kernel.cu:151-159,943).
+__global__ void __launch_bounds__(256) mh_xorwow_init_kernel(uint64_t seed, int64_t chain_offset,
+                                                             int64_t n, unsigned int* xw) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t g = (uint64_t)(chain_offset + c);
+    const CurandXorwowSeeder e((unsigned int)(seed + g), g);
+    e.store(xw + c * 6);
+}
+
+__global__ void mh_rng_xw_kernel(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
+                                 float* uni, float* nrm) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned int w[6];
+    CurandXorwowSeeder(seed, subsequence).store(w);
+    ChainRngXw r;
+    for (int pass = 0; pass < 3; ++pass) {
+        r.d = w[0];
+        r.x0 = w[1];
+        r.x1 = w[2];
+        r.x2 = w[3];
+        r.x3 = w[4];
+        r.x4 = w[5];
+        r.draws = 0;
+        r.bm_has = 0;
+        r.bm_val = 0.f;
+        for (int i = 0; i < n; ++i) {
+            if (pass == 0) u32[i] = r.next();
+            else if (pass == 1) uni[i] = r.uniform();
+            else nrm[i] = r.normal();
+        }
+    }
 }
 
 // ---- diagnostic: the group collectives on given lane values ---------------------------------
@@ -1167,6 +1238,7 @@ size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
 
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
+    if (op == OP_STEP && a.rng == RNG_CURAND_XORWOW) return launch_step_xw(a, L, npl, waves_per_wg, s);
     // (lanes per chain, objects per lane) instantiations; npl rounds up to the next one.
     switch (L) {
         case 8:
@@ -1216,10 +1288,61 @@ hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hi
     return hipGetLastError();
 }
 
-hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
-                      float* nrm, hipStream_t s) {
-    hipLaunchKernelGGL(mh_rng_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
+                      float* uni, float* nrm, hipStream_t s) {
+    if (kind == RNG_CURAND_XORWOW)
+        hipLaunchKernelGGL(mh_rng_xw_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+    else
+        hipLaunchKernelGGL(mh_rng_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+    return hipGetLastError();
+}
+
+hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mh_xorwow_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       seed, chain_offset, n, xw);
     return hipGetLastError();
 }
 
 }  // namespace mh
+#else  // MH_CHAIN_XW_TU: the step kernels drawing from the cuRAND XORWOW stream
+
+template <int L, int NPL>
+static hipError_t launch_geom_xw(const LaunchArgs& a, int waves_per_wg, hipStream_t stream) {
+    constexpr int G = 64 / L;
+    const int64_t chains_per_wg = (int64_t)waves_per_wg * G;
+    const int64_t blocks = (a.n_chains + chains_per_wg - 1) / chains_per_wg;
+    const size_t lds = (size_t)a.lay.hdr + (size_t)waves_per_wg * G * a.lay.stride;
+    hipLaunchKernelGGL((mh_kernel<L, NPL, OP_STEP_XW>), dim3((unsigned)blocks),
+                       dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_xw(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
+    switch (L) {
+        case 8:
+            if (npl <= 1) return launch_geom_xw<8, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_xw<8, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_xw<8, 4>(a, waves_per_wg, s);
+            return launch_geom_xw<8, 8>(a, waves_per_wg, s);
+        case 16:
+            if (npl <= 1) return launch_geom_xw<16, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_xw<16, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_xw<16, 4>(a, waves_per_wg, s);
+            return launch_geom_xw<16, 8>(a, waves_per_wg, s);
+        case 32:
+            if (npl <= 1) return launch_geom_xw<32, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_xw<32, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_xw<32, 4>(a, waves_per_wg, s);
+            return launch_geom_xw<32, 8>(a, waves_per_wg, s);
+        default:
+            if (npl <= 1) return launch_geom_xw<64, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_xw<64, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_xw<64, 4>(a, waves_per_wg, s);
+            return launch_geom_xw<64, 8>(a, waves_per_wg, s);
+    }
+}
+
+}  // namespace mh
+#endif  // MH_CHAIN_XW_TU

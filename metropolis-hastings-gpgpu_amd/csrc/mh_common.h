@@ -128,6 +128,98 @@ struct ChainRng {
     }
 };
 
+// cuRAND's Box-Muller for curandStateXORWOW (curand_normal -> _curand_box_muller): float
+// arithmetic on u = x * 2^-32 + 2^-33 and v = y * (2^-32 * 2pi_f) + half of that (one fma, as
+// nvcc contracts it by default), s = sqrtf(-2 logf(u)), (sin(v) * s, cos(v) * s). logf, sinf
+// and cosf are the double functions rounded once to float (the correctly rounded values but
+// for ~2^-29 of inputs); NVIDIA's device path uses the approximate __sincosf, so its normals
+// can differ in the last bits (DESIGN.md "RNG modes"). Out of line, like box_muller.
+static __device__ __attribute__((noinline)) float2 curand_box_muller(unsigned int x, unsigned int y) {
+    constexpr float kInv = 0x1p-32f;
+    constexpr float kInv2Pi = 0x1p-32f * 6.2831855f;  // CURAND_2POW32_INV_2PI (exact scaling)
+    const float u = (float)x * kInv + kInv * 0.5f;
+    const float v = __builtin_fmaf((float)y, kInv2Pi, kInv2Pi * 0.5f);
+    const float lg = (float)log((double)u);
+    const float s = __builtin_sqrtf(-2.0f * lg);
+    double sn, cs;
+    sincos((double)v, &sn, &cs);
+    return make_float2((float)sn * s, (float)cs * s);
+}
+
+// cuRAND XORWOW stream (curandStateXORWOW_t; the reference seeds thread tid with
+// curand_init(seed + tid, tid, 0), Kernel.cu:159,943): Marsaglia's xorshift over five words
+// plus a Weyl sequence, 2^67 draws per subsequence. Seeding and the subsequence jump happen
+// once per session in mh_xorwow_init_kernel; the state then lives in registers and is saved
+// after every launch. Same interface as ChainRng.
+struct ChainRngXw {
+    unsigned int d, x0, x1, x2, x3, x4;
+    uint64_t draws;
+    int bm_has;
+    float bm_val;
+
+    __device__ __forceinline__ unsigned int next() {
+        const unsigned int t = x0 ^ (x0 >> 2);
+        x0 = x1;
+        x1 = x2;
+        x2 = x3;
+        x3 = x4;
+        x4 = (x4 ^ (x4 << 4)) ^ (t ^ (t << 1));
+        d += 362437u;
+        ++draws;
+        return d + x4;
+    }
+    // curand_uniform (Kernel.cu:569,710): x * 2^-32 + 2^-33 in float, in (0, 1].
+    __device__ __forceinline__ float uniform() { return (float)next() * 0x1p-32f + 0x1p-33f; }
+    // curand_normal (Kernel.cu:605,608,641): sine branch first, cosine branch cached.
+    __device__ __forceinline__ float normal() {
+        if (bm_has) {
+            bm_has = 0;
+            return bm_val;
+        }
+        const unsigned int a = next();
+        const unsigned int b = next();
+        const float2 z = curand_box_muller(a, b);
+        bm_val = z.y;
+        bm_has = 1;
+        return z.x;
+    }
+};
+
+template <bool XW> struct RngOf { using type = ChainRng; };
+template <> struct RngOf<true> { using type = ChainRngXw; };
+
+// Resume / save a chain's stream around a launch. Philox resumes from the draw count; XORWOW
+// from its saved state words.
+__device__ __forceinline__ void rng_load(ChainRng& r, const LaunchArgs& a, int64_t chain,
+                                         const ChainMeta& m) {
+    r.init(a.seed, (uint64_t)(a.chain_offset + chain), m.draws);
+    r.bm_has = m.bm_has;
+    r.bm_val = m.bm_val;
+}
+__device__ __forceinline__ void rng_load(ChainRngXw& r, const LaunchArgs& a, int64_t chain,
+                                         const ChainMeta& m) {
+    const unsigned int* w = a.xw + chain * 6;
+    r.d = w[0];
+    r.x0 = w[1];
+    r.x1 = w[2];
+    r.x2 = w[3];
+    r.x3 = w[4];
+    r.x4 = w[5];
+    r.draws = m.draws;
+    r.bm_has = m.bm_has;
+    r.bm_val = m.bm_val;
+}
+__device__ __forceinline__ void rng_save(const ChainRng&, const LaunchArgs&, int64_t) {}
+__device__ __forceinline__ void rng_save(const ChainRngXw& r, const LaunchArgs& a, int64_t chain) {
+    unsigned int* w = a.xw + chain * 6;
+    w[0] = r.d;
+    w[1] = r.x0;
+    w[2] = r.x1;
+    w[3] = r.x2;
+    w[4] = r.x3;
+    w[5] = r.x4;
+}
+
 // ---- numerics shared by every term ---------------------------------------------------------
 
 // Kernel.cu:162-167: float difference, double root.
@@ -427,21 +519,24 @@ __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, dou
 
 // ---- proposal draws and the accept rule ----------------------------------------------------
 
-__device__ __forceinline__ int rand_int(ChainRng& rng, int max, int min) {
+template <class Rng>
+__device__ __forceinline__ int rand_int(Rng& rng, int max, int min) {
     float u = rng.uniform();
     u = (float)((double)u * ((double)(max - min) + 0.999999));
     u = u + (float)min;
     return (int)truncf(u);
 }
 
-__device__ __forceinline__ int pick_object(ChainRng& rng, int n, const unsigned char* frozen) {
+template <class Rng>
+__device__ __forceinline__ int pick_object(Rng& rng, int n, const unsigned char* frozen) {
     int k = rand_int(rng, n - 1, 0);
     while (frozen[k]) k = rand_int(rng, n - 1, 0);  // frozen[n] == 1: index n is redrawn
     return k;
 }
 
 // Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
-__device__ __forceinline__ bool accept(ChainRng& rng, float star, float cur) {
+template <class Rng>
+__device__ __forceinline__ bool accept(Rng& rng, float star, float cur) {
     const float u = rng.uniform();
     const float thr = fminf(1.0f, (float)exp(kBeta * ((double)star - (double)cur)));
     return u < thr;

@@ -434,7 +434,8 @@ __device__ __forceinline__ void write_pose(const DeltaPtrs& ch, int k, double x,
     p[2] = (float)ry;
 }
 
-__device__ int2 propose(ChainRng& rng, const DevRoom& rm, const unsigned char* frozen,
+template <class Rng>
+__device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen,
                         const DeltaPtrs& ch, bool writer) {
     const int n = rm.n;
     const int mode = rand_int(rng, 2, 0);
@@ -610,7 +611,7 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
 
 // ---- the kernel ---------------------------------------------------------------------------
 
-template <int L>
+template <int L, bool XW>
 __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / L;
@@ -737,10 +738,8 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     float cur_total = m0.costs[0];
     if (writer)
         for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
-    ChainRng rng;
-    rng.init(a.seed, (uint64_t)(a.chain_offset + cidx), m0.draws);
-    rng.bm_has = m0.bm_has;
-    rng.bm_val = m0.bm_val;
+    typename RngOf<XW>::type rng;
+    rng_load(rng, a, cidx, m0);
     uint64_t accepted = m0.accepted;
     float best_total = m0.best_total;
     double* best_dst = a.best + cidx * (int64_t)(F_COUNT * n);
@@ -843,6 +842,7 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         m.accepted = accepted;
         m.bm_has = rng.bm_has;
         m.bm_val = rng.bm_val;
+        rng_save(rng, a, chain);
         for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
         m.best_total = best_total;
         m.pad = 0;
@@ -864,8 +864,12 @@ hipError_t launch_delta_l(const LaunchArgs& a, int waves_per_wg, hipStream_t str
     const int64_t chains_per_wg = (int64_t)waves_per_wg * G;
     const int64_t blocks = (a.n_chains + chains_per_wg - 1) / chains_per_wg;
     const size_t lds = (size_t)a.dlay.hdr + (size_t)waves_per_wg * G * a.dlay.stride;
-    hipLaunchKernelGGL((mh_delta_kernel<L>), dim3((unsigned)blocks),
-                       dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
+    if (a.rng == RNG_CURAND_XORWOW)
+        hipLaunchKernelGGL((mh_delta_kernel<L, true>), dim3((unsigned)blocks),
+                           dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
+    else
+        hipLaunchKernelGGL((mh_delta_kernel<L, false>), dim3((unsigned)blocks),
+                           dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
     return hipGetLastError();
 }
 

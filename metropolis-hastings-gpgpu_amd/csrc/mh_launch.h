@@ -11,7 +11,10 @@
 
 namespace mh {
 
-enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3 };
+enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3, OP_STEP_XW = 4 };
+
+// Which stream the chains draw from (mh_options.rng).
+enum RngKind { RNG_PHILOX = 0, RNG_CURAND_XORWOW = 1 };
 
 struct LaunchArgs {
     DevRoom rm;
@@ -29,6 +32,8 @@ struct LaunchArgs {
     int iterations;
     int track;               // TRACK_OFF / TRACK_LOWEST / TRACK_HIGHEST
     double* best;            // [n_chains][6][N] best-of-chain configurations (track != 0)
+    int rng;                 // RngKind
+    unsigned int* xw;        // [n_chains][6] XORWOW states {d, x0..x4} (rng == RNG_CURAND_XORWOW)
     ChainLds lay;
     DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
 };
@@ -43,7 +48,10 @@ hipError_t launch_delta(const LaunchArgs& a, int L, int waves_per_wg, hipStream_
 hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
                           int64_t chain_offset, mh_summary* out, hipStream_t s);
 hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hipStream_t s);
-hipError_t launch_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* u32, float* uni,
-                      float* nrm, hipStream_t s);
+hipError_t launch_step_xw(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
+hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
+                      float* uni, float* nrm, hipStream_t s);
+hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
+                              hipStream_t s);
 
 }  // namespace mh

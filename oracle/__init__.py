@@ -56,6 +56,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
     lib.orc_philox4x32_10.restype = None
     lib.orc_rng_init.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+    lib.orc_rng_init_xorwow.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int]
+    lib.orc_rng_init_xorwow.restype = None
     lib.orc_rng_next.argtypes = [C.c_void_p]
     lib.orc_rng_next.restype = C.c_uint32
     lib.orc_rng_uniform.argtypes = [C.c_void_p]
@@ -89,7 +91,11 @@ class OrcRoom(C.Structure):
 
 class OrcRng(C.Structure):
     _fields_ = [("counter", C.c_uint32 * 4), ("result", C.c_uint32 * 4), ("key", C.c_uint32 * 2),
-                ("substate", C.c_uint32), ("bm_has", C.c_int32), ("bm_val", C.c_float)]
+                ("substate", C.c_uint32), ("bm_has", C.c_int32), ("bm_val", C.c_float),
+                ("kind", C.c_int32), ("xw", C.c_uint32 * 6)]
+
+
+PHILOX, XORWOW_CURAND, XORWOW_ROCRAND = 0, 1, 2
 
 
 def orc_room(room) -> OrcRoom:
@@ -112,23 +118,25 @@ def costs(room, cfg=None) -> np.ndarray:
 
 
 class OrcOptions(C.Structure):  # mh_options, include/mh_kernel.h
-    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("reserved", C.c_int32 * 5)]
+    _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("rng", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int = 0,
-               threads: int = 1, state: bool = False, track: int = 0):
+               threads: int = 1, state: bool = False, track: int = 0, rng: int = 0):
     """Runs the restated chain loop. Returns (points [chains,N,6] float32 or state
     [chains,N,6] float64 (x,y,z,rotX,rotY,rotZ), costs [chains,8] float32, accepted [chains]
     int64). `track` = 1 / 2 returns each chain's lowest / highest-total configuration instead
-    of its final one (the reference's commented-out cfgBest, Kernel.cu:779-816)."""
+    of its final one (the reference's commented-out cfgBest, Kernel.cu:779-816). `rng` = 1
+    draws from cuRAND's XORWOW seeded as the reference seeds it (mh_options.rng)."""
     lib = load()
     n = room.n
     cs = (C.c_float * (8 * chains))()
     acc = (C.c_int64 * chains)()
-    if track:
+    if track or rng:
         state = True
         buf = (C.c_uint8 * (72 * n * chains))()
-        opts = OrcOptions(seed, track)
+        opts = OrcOptions(seed, track, rng)
         rc = lib.orc_run_chains_ex(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p),
                                    C.byref(opts), chain_begin, chains, iterations, threads,
                                    C.cast(buf, C.c_void_p), C.cast(cs, C.c_void_p), acc)
@@ -156,14 +164,23 @@ def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int =
     return np.frombuffer(bytes(buf), dtype=np.float32).reshape(chains, n, 6).copy(), c8, a
 
 
-def rng_streams(seed: int, subsequence: int, n: int):
-    """(u32, uniform, normal) streams, each restarted at draw 0 (as mh_debug_rng)."""
+def rng_init(seed: int, subsequence: int, kind: int = PHILOX) -> OrcRng:
     lib = load()
-    u = (C.c_uint32 * n)()
-    lib.orc_philox_stream(seed, subsequence, u, n)
     r = OrcRng()
-    lib.orc_rng_init(C.byref(r), seed, subsequence)
+    if kind == PHILOX:
+        lib.orc_rng_init(C.byref(r), seed, subsequence)
+    else:
+        lib.orc_rng_init_xorwow(C.byref(r), seed, subsequence, kind)
+    return r
+
+
+def rng_streams(seed: int, subsequence: int, n: int, kind: int = PHILOX):
+    """(u32, uniform, normal) streams, each restarted at draw 0 (as mh_debug_rng_ex)."""
+    lib = load()
+    r = rng_init(seed, subsequence, kind)
+    u = np.array([lib.orc_rng_next(C.byref(r)) for _ in range(n)], dtype=np.uint32)
+    r = rng_init(seed, subsequence, kind)
     f = np.array([lib.orc_rng_uniform(C.byref(r)) for _ in range(n)], dtype=np.float32)
-    lib.orc_rng_init(C.byref(r), seed, subsequence)
+    r = rng_init(seed, subsequence, kind)
     g = np.array([lib.orc_rng_normal(C.byref(r)) for _ in range(n)], dtype=np.float32)
-    return np.frombuffer(bytes(u), dtype=np.uint32).copy(), f, g
+    return u, f, g

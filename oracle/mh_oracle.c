@@ -90,7 +90,122 @@ void orc_rng_init(orc_rng* r, uint64_t seed, uint64_t subsequence) {
     rng_refill(r);
 }
 
+/* ------------------------------------------------------------------------------------------
+ * cuRAND XORWOW (curandStateXORWOW_t; Kernel.cu:19 includes curand_kernel.h and :159 seeds
+ * thread tid with curand_init(seed + tid, tid, 0)). cuRAND is not in this image; its published
+ * algorithm is restated here: Marsaglia's xorwow (five xorshift words plus a Weyl sequence
+ * d += 362437, output d + x4), seeded by scrambling the two 32-bit halves of the seed, with
+ * subsequences 2^67 draws apart. The jump is computed here independently, as powers of the
+ * 160 x 160 GF(2) transition matrix (the Weyl word needs no jump: 362437 * 2^67 = 0 mod 2^32).
+ * ---------------------------------------------------------------------------------------- */
+static void xw_step(uint32_t x[5]) {
+    const uint32_t t = x[0] ^ (x[0] >> 2);
+    x[0] = x[1];
+    x[1] = x[2];
+    x[2] = x[3];
+    x[3] = x[4];
+    x[4] = (x[4] ^ (x[4] << 4)) ^ (t ^ (t << 1));
+}
+
+/* Column k of a matrix is the image of basis vector e_k (word k / 32, bit k % 32). */
+typedef struct { uint32_t col[160][5]; } xw_mat;
+
+static void xw_apply(const xw_mat* m, const uint32_t v[5], uint32_t out[5]) {
+    uint32_t o[5] = {0, 0, 0, 0, 0};
+    for (int k = 0; k < 160; ++k)
+        if ((v[k >> 5] >> (k & 31)) & 1u)
+            for (int w = 0; w < 5; ++w) o[w] ^= m->col[k][w];
+    memcpy(out, o, sizeof o);
+}
+
+static void xw_mul(const xw_mat* a, const xw_mat* b, xw_mat* out) { /* out = a * b */
+    for (int k = 0; k < 160; ++k) xw_apply(a, b->col[k], out->col[k]);
+}
+
+static xw_mat g_xw_seq[64]; /* g_xw_seq[j] = A^(2^(67 + j)) */
+static pthread_once_t g_xw_once = PTHREAD_ONCE_INIT;
+
+static void xw_build_tables(void) {
+    xw_mat* m = malloc(sizeof *m);
+    xw_mat* t = malloc(sizeof *t);
+    for (int k = 0; k < 160; ++k) {
+        uint32_t e[5] = {0, 0, 0, 0, 0};
+        e[k >> 5] = 1u << (k & 31);
+        xw_step(e);
+        memcpy(m->col[k], e, sizeof e);
+    }
+    for (int i = 0; i < 67; ++i) { /* A^(2^67) */
+        xw_mul(m, m, t);
+        memcpy(m, t, sizeof *m);
+    }
+    g_xw_seq[0] = *m;
+    for (int j = 1; j < 64; ++j) xw_mul(&g_xw_seq[j - 1], &g_xw_seq[j - 1], &g_xw_seq[j]);
+    free(m);
+    free(t);
+}
+
+void orc_rng_init_xorwow(orc_rng* r, uint64_t seed, uint64_t subsequence, int kind) {
+    memset(r, 0, sizeof *r);
+    r->kind = kind;
+    uint32_t s0, s1, t0, t1;
+    if (kind == ORC_XORWOW_ROCRAND) { /* rocrand_xorwow.h xorwow_engine(seed, subsequence, 0) */
+        s0 = (uint32_t)seed ^ 0x2c7f967fu;
+        s1 = (uint32_t)(seed >> 32) ^ 0xa03697cbu;
+        t0 = 1228688033u * s0;
+        t1 = 2073658381u * s1;
+    } else { /* cuRAND _curand_init_scratch */
+        s0 = (uint32_t)seed ^ 0xaad26b49u;
+        s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+        t0 = 1099087573u * s0;
+        t1 = 2591861531u * s1;
+    }
+    uint32_t* x = r->xw + 1;
+    r->xw[0] = 6615241u + t1 + t0;
+    x[0] = 123456789u + t0;
+    x[1] = 362436069u ^ t0;
+    x[2] = 521288629u + t1;
+    x[3] = 88675123u ^ t1;
+    x[4] = 5783321u + t0;
+    pthread_once(&g_xw_once, xw_build_tables);
+    for (int j = 0; j < 64; ++j)
+        if ((subsequence >> j) & 1u) xw_apply(&g_xw_seq[j], x, x);
+}
+
+static uint32_t xw_next(orc_rng* r) {
+    xw_step(r->xw + 1);
+    r->xw[0] += 362437u;
+    return r->xw[0] + r->xw[5];
+}
+
+/* curand_uniform: x * 2^-32 + 2^-33 in float (Kernel.cu:569,710). */
+static float xw_uniform(orc_rng* r) {
+    float v = (float)xw_next(r);
+    float scaled = v * 0x1p-32f;
+    return scaled + 0x1p-33f;
+}
+
+/* curand_normal -> _curand_box_muller: u = x 2^-32 + 2^-33, v = fma(y, 2^-32 2pi_f, half of
+ * it), s = sqrtf(-2 logf(u)), (sinf(v) s, cosf(v) s); sine branch first, cosine cached. The
+ * float transcendentals are the double functions rounded once (see DESIGN.md "RNG modes"). */
+static float xw_normal(orc_rng* r) {
+    if (r->bm_has) {
+        r->bm_has = 0;
+        return r->bm_val;
+    }
+    const uint32_t a = xw_next(r), b = xw_next(r);
+    const float k2pi = 0x1p-32f * 6.2831855f;
+    const float u = (float)a * 0x1p-32f + 0x1p-33f;
+    const float v = fmaf((float)b, k2pi, k2pi * 0.5f);
+    const float lg = (float)log((double)u);
+    const float s = sqrtf(-2.0f * lg);
+    const float sn = (float)sin((double)v), cs = (float)cos((double)v);
+    r->bm_val = cs * s;
+    r->bm_has = 1;
+    return sn * s;
+}
+
 uint32_t orc_rng_next(orc_rng* r) {
+    if (r->kind) return xw_next(r);
     uint32_t v = r->result[r->substate];
     if (++r->substate == 4) {
         r->substate = 0;
@@ -103,6 +218,7 @@ uint32_t orc_rng_next(orc_rng* r) {
 /* rocrand_uniform (rocrand_uniform.h uniform_distribution): (0, 1], float arithmetic. Plays
  * the role of curand_uniform at Kernel.cu:569,710. */
 float orc_rng_uniform(orc_rng* r) {
+    if (r->kind) return xw_uniform(r);
     const float inv = 2.3283064e-10f;
     float v = (float)orc_rng_next(r);
     float scaled = v * inv;
@@ -113,6 +229,7 @@ float orc_rng_uniform(orc_rng* r) {
  * uniforms in (0,1) evaluated in double and rounded to float; the sine branch is returned
  * first and the cosine branch is cached for the next call, as cuRAND's Box-Muller does. */
 float orc_rng_normal(orc_rng* r) {
+    if (r->kind) return xw_normal(r);
     if (r->bm_has) {
         r->bm_has = 0;
         return r->bm_val;
@@ -527,6 +644,7 @@ typedef struct {
     int64_t lo, hi; /* local chain range for this worker */
     int iterations;
     int track; /* MH_TRACK_* */
+    int rng;   /* MH_RNG_* */
     point* out_points;
     positionAndRotation* out_state;
     resultCosts* out_costs;
@@ -537,7 +655,11 @@ static void run_one(const chain_job* job, int64_t local, positionAndRotation* cu
                     positionAndRotation* star, positionAndRotation* best) {
     const int n = job->room->srf->nObjs;
     orc_rng r;
-    orc_rng_init(&r, job->seed, (uint64_t)(job->chain_begin + local));
+    const uint64_t gid = (uint64_t)(job->chain_begin + local);
+    if (job->rng == MH_RNG_CURAND_XORWOW) /* curand_init(seed + tid, tid, 0), Kernel.cu:159 */
+        orc_rng_init_xorwow(&r, (uint32_t)(job->seed + gid), gid, ORC_XORWOW_CURAND);
+    else
+        orc_rng_init(&r, job->seed, gid);
     memcpy(cur, job->cfg, sizeof(positionAndRotation) * n);
     resultCosts cc, sc;
     orc_costs(job->room, cur, &cc);
@@ -592,13 +714,14 @@ static void* chain_worker(void* arg) {
 }
 
 static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
-                      int track, int64_t chain_begin, int64_t n_chains, int iterations,
+                      int track, int rng, int64_t chain_begin, int64_t n_chains, int iterations,
                       int nthreads,
                       point* out_points, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted) {
     if (orc_validate(room, cfg) != 0) return -1;
     if (n_chains < 0 || iterations < 0) return fail("negative chain or step count%ld", 0);
     if (track < MH_TRACK_OFF || track > MH_TRACK_HIGHEST) return fail("bad track_best %ld", track);
+    if (rng < MH_RNG_PHILOX || rng > MH_RNG_CURAND_XORWOW) return fail("bad rng %ld", rng);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > n_chains) nthreads = (int)(n_chains > 0 ? n_chains : 1);
     chain_job* jobs = calloc((size_t)nthreads, sizeof(chain_job));
@@ -606,7 +729,7 @@ static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint
     for (int t = 0; t < nthreads; ++t) {
         chain_job j = {room, cfg, seed, chain_begin,
                        n_chains * t / nthreads, n_chains * (t + 1) / nthreads,
-                       iterations, track, out_points, out_state, out_costs, out_accepted};
+                       iterations, track, rng, out_points, out_state, out_costs, out_accepted};
         jobs[t] = j;
     }
     for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, chain_worker, &jobs[t]);
@@ -620,22 +743,22 @@ static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint
 int orc_run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                    int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                    point* out_points, resultCosts* out_costs, int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, MH_TRACK_OFF, chain_begin, n_chains, iterations, nthreads,
-                      out_points, NULL, out_costs, out_accepted);
+    return run_chains(room, cfg, seed, MH_TRACK_OFF, MH_RNG_PHILOX, chain_begin, n_chains,
+                      iterations, nthreads, out_points, NULL, out_costs, out_accepted);
 }
 
 int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                          int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                          positionAndRotation* out_state, resultCosts* out_costs,
                          int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, MH_TRACK_OFF, chain_begin, n_chains, iterations, nthreads,
-                      NULL, out_state, out_costs, out_accepted);
+    return run_chains(room, cfg, seed, MH_TRACK_OFF, MH_RNG_PHILOX, chain_begin, n_chains,
+                      iterations, nthreads, NULL, out_state, out_costs, out_accepted);
 }
 
 int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       const mh_options* opts, int64_t chain_begin, int64_t n_chains,
                       int iterations, int nthreads, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted) {
-    return run_chains(room, cfg, opts->seed, opts->track_best, chain_begin, n_chains, iterations,
-                      nthreads, NULL, out_state, out_costs, out_accepted);
+    return run_chains(room, cfg, opts->seed, opts->track_best, opts->rng, chain_begin, n_chains,
+                      iterations, nthreads, NULL, out_state, out_costs, out_accepted);
 }

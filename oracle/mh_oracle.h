@@ -42,7 +42,15 @@ typedef struct orc_rng {
     uint32_t substate;
     int32_t bm_has;
     float bm_val;
+    int32_t kind;    /* 0 Philox; ORC_XORWOW_CURAND / ORC_XORWOW_ROCRAND: the xorwow below */
+    uint32_t xw[6];  /* xorwow {d, x0..x4} */
 } orc_rng;
+
+/* XORWOW seeding constants: cuRAND's (the reference's generator, Kernel.cu:19,159) or
+ * rocRAND's (rocrand_xorwow.h; used only to pin the recurrence and the subsequence jump against
+ * rocRAND's own engine, tests/golden/xorwow_rocrand.cpp). */
+#define ORC_XORWOW_CURAND 1
+#define ORC_XORWOW_ROCRAND 2
 
 /* 0 on success, negative on a validation error (message via orc_last_error). */
 int orc_validate(const orc_room* room, const positionAndRotation* cfg);
@@ -67,6 +75,10 @@ uint32_t orc_rng_next(orc_rng* r);
 float orc_rng_uniform(orc_rng* r);
 float orc_rng_normal(orc_rng* r);
 void orc_philox_stream(uint64_t seed, uint64_t subsequence, uint32_t* out, int n);
+/* curand_init(seed, subsequence, 0) for a curandStateXORWOW (kind ORC_XORWOW_CURAND), or the
+ * rocRAND engine's equivalent (ORC_XORWOW_ROCRAND). orc_rng_next / _uniform / _normal then draw
+ * curand(), curand_uniform() and curand_normal(). */
+void orc_rng_init_xorwow(orc_rng* r, uint64_t seed, uint64_t subsequence, int kind);
 /* Random123 philox4x32 with 10 rounds on one (counter, key) block, for KAT vectors. */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
@@ -98,6 +110,8 @@ int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, u
 /* orc_run_chains_state with the options of KernelWrapperEx (include/mh_kernel.h): seed and
  * best-of-chain tracking. With tracking on, out_state / out_costs hold each chain's best
  * configuration and its costs. */
+/* opts->rng == MH_RNG_CURAND_XORWOW: chain c draws from curand_init((uint32_t)(seed + c), c, 0)
+ * as Kernel.cu:151-159,943 seeds thread c. */
 int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       const mh_options* opts, int64_t chain_begin, int64_t n_chains,
                       int iterations, int nthreads, positionAndRotation* out_state,

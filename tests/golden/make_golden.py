@@ -8,13 +8,19 @@
 * chains: hashes of the oracle's final poses/costs for seeded runs of the defined chain on the
   main() room and synthetic rooms; the HIP path must reproduce them bit for bit.
 * rooms: hashes of the synthetic rooms' wire bytes (SURVEY.md 8(d) generator).
+* xorwow_rocrand: the first draws of rocRAND's own XORWOW engine (xorwow_rocrand.cpp, built here
+  with hipcc for the host) -- pins the oracle's XORWOW recurrence and subsequence jump.
+* xorwow_curand / chains_xorwow: the oracle's cuRAND-XORWOW streams and seeded chain runs in
+  that mode (the HIP path must reproduce them bit for bit).
 
 Run from the repo root:  python tests/golden/make_golden.py
 """
 import ctypes as C
 import hashlib
 import json
+import subprocess
 import sys
+import tempfile
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
@@ -29,6 +35,20 @@ CHAIN_CASES = [
     {"room": "synthetic_frozen", "n": 16, "chains": 64, "steps": 200, "seed": 11},
 ]
 RNG_CASES = [(42, 0), (42, 65535), (2**63 + 5, 123456789)]
+XORWOW_CASES = [(1760000000, 0), (1760000000 + 4097, 4097), (7, 2**40 + 3)]
+XORWOW_CHAIN_CASES = [
+    {"room": "main_fixture", "n": 32, "chains": 64, "steps": 40, "seed": 1760000000},
+    {"room": "synthetic", "n": 64, "chains": 16, "steps": 100, "seed": 42},
+]
+
+
+def rocrand_xorwow_vectors():
+    src = Path(__file__).with_name("xorwow_rocrand.cpp")
+    with tempfile.TemporaryDirectory() as d:
+        exe = Path(d) / "xorwow_rocrand"
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O1", str(src), "-o", str(exe)], check=True)
+        return json.loads(subprocess.run([str(exe)], check=True, capture_output=True,
+                                         text=True).stdout)
 
 
 def make_room(mh, case):
@@ -71,6 +91,22 @@ def main():
         out["chains"].append(dict(case, points_sha256=sha(pts), costs_sha256=sha(costs),
                                   mean_total=float(costs[:, 0].astype("float64").mean()),
                                   accepted=int(acc.sum())))
+    out["xorwow_rocrand"] = rocrand_xorwow_vectors()
+    out["xorwow_curand"] = []
+    for seed, sub in XORWOW_CASES:
+        u, f, g = orc.rng_streams(seed, sub, 16, kind=orc.XORWOW_CURAND)
+        out["xorwow_curand"].append({"seed": seed, "subsequence": sub, "u32": [int(x) for x in u],
+                                     "uniform_bits": [int(x) for x in f.view("uint32")],
+                                     "normal_bits": [int(x) for x in g.view("uint32")]})
+    out["chains_xorwow"] = []
+    for case in XORWOW_CHAIN_CASES:
+        room = make_room(mh, case)
+        st, costs, acc = orc.run_chains(room, case["chains"], case["steps"], case["seed"],
+                                        threads=8, rng=1)
+        pts = st.astype("float32")
+        out["chains_xorwow"].append(dict(case, points_sha256=sha(pts), costs_sha256=sha(costs),
+                                         mean_total=float(costs[:, 0].astype("float64").mean()),
+                                         accepted=int(acc.sum())))
     out["rooms"] = {f"synthetic{n}": hashlib.sha256(room_bytes(mh.synthetic_room(n))).hexdigest()
                     for n in (1, 8, 64, 256)}
     path = Path(__file__).with_name("golden.json")

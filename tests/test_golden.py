@@ -49,3 +49,33 @@ def test_golden_rooms(mh, n):
     w = room.surface_rectangle[0].x
     base = np.ctypeslib.as_array(room.cfg)
     assert np.all((base["x"] >= 0) & (base["x"] <= w) & (base["y"] >= 0) & (base["y"] <= w))
+
+
+@pytest.mark.parametrize("case", GOLDEN["xorwow_rocrand"],
+                         ids=lambda c: f"{c['seed']}-{c['subsequence']}")
+def test_oracle_xorwow_matches_rocrand_engine(orc, case):
+    """The oracle's XORWOW (its own GF(2) subsequence jump) run with rocRAND's seeding constants
+    reproduces rocRAND's xorwow_engine (tests/golden/xorwow_rocrand.cpp): the recurrence, the
+    Weyl sequence and the 2^67-draw jump it shares with cuRAND are pinned; only the seeding
+    constants differ between the two libraries."""
+    u, _, _ = orc.rng_streams(case["seed"], case["subsequence"], 8, kind=orc.XORWOW_ROCRAND)
+    assert [int(x) for x in u] == case["u32"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["xorwow_curand"],
+                         ids=lambda c: f"{c['seed']}-{c['subsequence']}")
+def test_golden_xorwow_curand(orc, case):
+    u, f, g = orc.rng_streams(case["seed"], case["subsequence"], 16, kind=orc.XORWOW_CURAND)
+    assert [int(x) for x in u] == case["u32"]
+    assert [int(x) for x in f.view(np.uint32)] == case["uniform_bits"]
+    assert [int(x) for x in g.view(np.uint32)] == case["normal_bits"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["chains_xorwow"], ids=lambda c: f"{c['room']}{c['n']}")
+def test_golden_chains_xorwow_oracle(mh, orc, case):
+    room = make_golden.make_room(mh, case)
+    st, costs, acc = orc.run_chains(room, case["chains"], case["steps"], case["seed"], threads=8,
+                                    rng=1)
+    assert make_golden.sha(st.astype(np.float32)) == case["points_sha256"]
+    assert make_golden.sha(costs) == case["costs_sha256"]
+    assert int(acc.sum()) == case["accepted"]

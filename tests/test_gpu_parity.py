@@ -408,3 +408,73 @@ def test_best_of_chain_full_size(mh, hiplib):
     fresh = mh.evaluate_costs(room, cfgs)
     rel = np.abs(fresh[:, 0] - costs[idx, 0]) / np.maximum(np.abs(costs[idx, 0]), 1)
     assert np.median(rel) < 1e-3
+
+
+# ---- cuRAND-XORWOW mode (mh_options.rng = MH_RNG_CURAND_XORWOW) ------------------------------
+
+@pytest.mark.parametrize("case", GOLDEN["xorwow_curand"],
+                         ids=lambda c: f"{c['seed']}-{c['subsequence']}")
+def test_xorwow_streams_hip(mh, hiplib, case):
+    """Device curand()/curand_uniform()/curand_normal() streams of curand_init(seed, sub, 0)
+    (rocRAND's subsequence jump under cuRAND's seeding) equal the oracle's restatement (its own
+    GF(2) jump), bit for bit."""
+    u, f, g = mh.debug_rng(case["seed"], case["subsequence"], 16, rng=1)
+    assert [int(x) for x in u] == case["u32"]
+    assert [int(x) for x in f.view(np.uint32)] == case["uniform_bits"]
+    assert [int(x) for x in g.view(np.uint32)] == case["normal_bits"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["chains_xorwow"], ids=lambda c: f"{c['room']}{c['n']}")
+def test_golden_chains_xorwow_hip(mh, hiplib, case):
+    room = MAKE_GOLDEN.make_room(mh, case)
+    pts, costs = mh.kernel_wrapper(room, case["chains"], case["steps"], seed=case["seed"], rng=1)
+    assert MAKE_GOLDEN.sha(pts) == case["points_sha256"]
+    assert MAKE_GOLDEN.sha(costs) == case["costs_sha256"]
+
+
+@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("kind,n,chains,steps", [
+    ("main", 32, 128, 300),
+    ("frozen", 16, 128, 400),
+    ("syn", 9, 256, 500),
+    ("syn", 64, 64, 1200),   # two launches: the XORWOW state is saved and resumed
+    ("syn", 100, 16, 120),
+])
+def test_xorwow_chains_match_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, chains, steps):
+    """Chains seeded exactly as the reference seeds them (curand_init(seed + c, c, 0),
+    Kernel.cu:159,943) against the oracle, bit for bit, for both step kernels."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    room = _room(mh, kind, n)
+    seed = 1760000000 + n
+    with mh.Session(room, chains, seed=seed, rng=1) as s:
+        assert s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_state, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8, rng=1)
+    ref_pts = ref_state.astype(np.float32)
+    same = np.all(pts.view(np.uint32) == ref_pts.view(np.uint32), axis=(1, 2)) & np.all(
+        costs.view(np.uint32) == ref_costs.view(np.uint32), axis=1)
+    print(f"xorwow {step} {kind} N={n}: {same.mean() * 100:.2f}% of chains bit-identical")
+    assert same.mean() >= 0.99
+
+
+def test_xorwow_sharded_sessions_equal_one(mh, hiplib):
+    """Chain c's XORWOW stream depends only on its global id: two sessions over [0, 96) and
+    [96, 256) reproduce one session over [0, 256) (the multi-GPU sharding invariant)."""
+    room = mh.synthetic_room(16)
+    seed, steps = 99, 300
+    with mh.Session(room, 256, seed=seed, rng=1, track=2) as s:
+        s.run(steps)
+        s.finalize()
+        p_all, c_all = s.download()
+    parts = []
+    for off, cnt in ((0, 96), (96, 160)):
+        with mh.Session(room, cnt, seed=seed, rng=1, track=2, chain_offset=off) as s:
+            s.run(steps)
+            s.finalize()
+            parts.append(s.download())
+    assert np.array_equal(np.concatenate([p[0] for p in parts]).view(np.uint32),
+                          p_all.view(np.uint32))
+    assert np.array_equal(np.concatenate([p[1] for p in parts]).view(np.uint32),
+                          c_all.view(np.uint32))

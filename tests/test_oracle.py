@@ -314,3 +314,32 @@ def test_best_of_chain_bounds(mh, orc):
             cfg[i].x, cfg[i].y, cfg[i].z, cfg[i].rotX, cfg[i].rotY, cfg[i].rotZ = hi_s[c, i]
             assert cfg[i].frozen == base[i]["frozen"]
         assert np.array_equal(orc.costs(room, cfg).view(np.uint32), hi[c].view(np.uint32))
+
+
+def test_xorwow_curand_formulas(orc):
+    """cuRAND XORWOW restated by hand: _curand_init_scratch's seeding of seed 0, one step of the
+    recurrence plus the Weyl sequence, and curand_uniform = x * 2^-32 + 2^-33 in float.
+    (The subsequence jump is pinned against rocRAND's engine in test_golden.py.)"""
+    lib = orc.load()
+    r = orc.rng_init(123, 0, orc.XORWOW_CURAND)
+    d, x = r.xw[0], list(r.xw)[1:]
+    v = lib.orc_rng_next(C.byref(r))
+    t = (x[0] ^ (x[0] >> 2)) & 0xffffffff
+    x4 = (x[4] ^ (x[4] << 4) ^ t ^ (t << 1)) & 0xffffffff
+    assert v == (d + 362437 + x4) & 0xffffffff
+    r = orc.rng_init(123, 0, orc.XORWOW_CURAND)
+    w = lib.orc_rng_next(C.byref(r))
+    r = orc.rng_init(123, 0, orc.XORWOW_CURAND)
+    assert lib.orc_rng_uniform(C.byref(r)) == np.float32(np.float32(w) * np.float32(2**-32) +
+                                                          np.float32(2**-33))
+    a = orc.rng_init(5, 3, orc.XORWOW_CURAND)
+    b = orc.rng_init(5, 1, orc.XORWOW_CURAND)
+    c = orc.rng_init(5, 2, orc.XORWOW_CURAND)
+    assert list(a.xw) != list(b.xw) != list(c.xw)
+    # cuRAND seeding of seed 0 by hand (_curand_init_scratch)
+    z = orc.rng_init(0, 0, orc.XORWOW_CURAND)
+    t0 = (1099087573 * 0xaad26b49) & 0xffffffff
+    t1 = (2591861531 * 0xf7dcefdd) & 0xffffffff
+    assert list(z.xw) == [(6615241 + t1 + t0) & 0xffffffff, (123456789 + t0) & 0xffffffff,
+                          362436069 ^ t0, (521288629 + t1) & 0xffffffff, 88675123 ^ t1,
+                          (5783321 + t0) & 0xffffffff]
