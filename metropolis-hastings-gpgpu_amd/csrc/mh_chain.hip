@@ -937,7 +937,6 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         rng_load(rng, a, chain, m0);
         uint64_t accepted = m0.accepted;
         float best_total = m0.best_total;
-        double* best_dst = a.best + chain * (int64_t)(F_COUNT * n);
         eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
 #if MH_STAMPS
         if (writer)
@@ -957,7 +956,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
                 best_total = sc[0];
-                save_best(ch, best_dst, n, r, L);
+                save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
             }
             if (accept(rng, sc[0], cur_total)) {
                 cur_total = sc[0];

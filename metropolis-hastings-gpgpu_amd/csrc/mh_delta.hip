@@ -742,7 +742,6 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     rng_load(rng, a, cidx, m0);
     uint64_t accepted = m0.accepted;
     float best_total = m0.best_total;
-    double* best_dst = a.best + cidx * (int64_t)(F_COUNT * n);
     int rc = 0;  // which RM buffer holds the current rows
 #if MH_STAMPS
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last;
@@ -802,7 +801,7 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
         if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
             best_total = sc[0];
-            if (live) save_best(ch, best_dst, n, r, L);
+            if (live) save_best(ch, a.best + cidx * (int64_t)(F_COUNT * n), n, r, L);
         }
         if (accept(rng, sc[0], cur_total)) {
             cur_total = sc[0];
