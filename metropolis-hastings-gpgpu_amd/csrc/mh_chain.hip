@@ -34,10 +34,12 @@
 #define MH_STAMPS 0  // diagnostic builds (tools/build_stamps.sh) time each phase; product = 0
 #endif
 
-#if MH_STAMPS && !defined(MH_CHAIN_XW_TU)
+#if MH_STAMPS
+#ifdef MH_CHAIN_XW_TU
+static __device__ unsigned long long g_phase_cycles[16];  // (XORWOW kernels: not reported)
+#else
 __device__ unsigned long long g_phase_cycles[16];
-#elif MH_STAMPS
-extern __device__ unsigned long long g_phase_cycles[16];
+#endif
 #define MH_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define MH_PHASE(ch, k, t0) do { unsigned long long _t; MH_STAMP(_t); (ch).aux->cyc[k] += _t - (t0); (t0) = _t; } while (0)
 #else
