@@ -21,7 +21,7 @@
 #include <stdlib.h>
 
 #include "mh_common.h"
-#ifndef MH_CHAIN_XW_TU
+#ifndef MH_CHAIN_STEP_TU
 #include <rocrand/rocrand_xorwow.h>
 #endif
 #ifndef MH_DOUBLE
@@ -35,7 +35,7 @@
 #endif
 
 #if MH_STAMPS
-#ifdef MH_CHAIN_XW_TU
+#ifdef MH_CHAIN_STEP_TU
 static __device__ unsigned long long g_phase_cycles[16];  // (XORWOW kernels: not reported)
 #else
 __device__ unsigned long long g_phase_cycles[16];
@@ -826,8 +826,10 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
 template <int L, int NPL, int OP>
 __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    // OP_STEP_XW: OP_STEP drawing from the cuRAND XORWOW stream instead of Philox.
-    constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_XW);
+    // OP_STEP_T: OP_STEP with best-of-chain tracking compiled in; OP_STEP_XW: the same drawing
+    // from the cuRAND XORWOW stream instead of Philox. Plain OP_STEP carries no tracking code.
+    constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_T || OP == OP_STEP_XW);
+    constexpr bool TRACK = (OP == OP_STEP_T || OP == OP_STEP_XW);
     using Rng = typename RngOf<OP == OP_STEP_XW>::type;
     constexpr int G = 64 / L;
     const int n = a.rm.n;
@@ -956,9 +958,11 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y);
             MH_STAMP(ts);
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
-            if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
-                best_total = sc[0];
-                save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
+            if constexpr (TRACK) {
+                if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
+                    best_total = sc[0];
+                    save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
+                }
             }
             if (accept(rng, sc[0], cur_total)) {
                 cur_total = sc[0];
@@ -1035,7 +1039,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     }
 }
 
-#ifndef MH_CHAIN_XW_TU
+#ifndef MH_CHAIN_STEP_TU
 // ---- summary reduction (for the multi-GPU best-cost all-gather) ---------------------------
 
 __global__ void __launch_bounds__(1024) mh_summary_kernel(const resultCosts* costs,
@@ -1240,6 +1244,7 @@ size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
     if (op == OP_STEP && a.rng == RNG_CURAND_XORWOW) return launch_step_xw(a, L, npl, waves_per_wg, s);
+    if (op == OP_STEP && a.track != TRACK_OFF) return launch_step_best(a, L, npl, waves_per_wg, s);
     // (lanes per chain, objects per lane) instantiations; npl rounds up to the next one.
     switch (L) {
         case 8:
@@ -1307,43 +1312,43 @@ hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, un
 }
 
 }  // namespace mh
-#else  // MH_CHAIN_XW_TU: the step kernels drawing from the cuRAND XORWOW stream
+#else  // MH_CHAIN_STEP_TU: one more family of step kernels (mh_chain_xw.hip, mh_chain_best.hip)
 
 template <int L, int NPL>
-static hipError_t launch_geom_xw(const LaunchArgs& a, int waves_per_wg, hipStream_t stream) {
+static hipError_t launch_geom_step(const LaunchArgs& a, int waves_per_wg, hipStream_t stream) {
     constexpr int G = 64 / L;
     const int64_t chains_per_wg = (int64_t)waves_per_wg * G;
     const int64_t blocks = (a.n_chains + chains_per_wg - 1) / chains_per_wg;
     const size_t lds = (size_t)a.lay.hdr + (size_t)waves_per_wg * G * a.lay.stride;
-    hipLaunchKernelGGL((mh_kernel<L, NPL, OP_STEP_XW>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((mh_kernel<L, NPL, MH_CHAIN_STEP_TU>), dim3((unsigned)blocks),
                        dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_step_xw(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
+hipError_t MH_CHAIN_STEP_LAUNCH(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     switch (L) {
         case 8:
-            if (npl <= 1) return launch_geom_xw<8, 1>(a, waves_per_wg, s);
-            if (npl <= 2) return launch_geom_xw<8, 2>(a, waves_per_wg, s);
-            if (npl <= 4) return launch_geom_xw<8, 4>(a, waves_per_wg, s);
-            return launch_geom_xw<8, 8>(a, waves_per_wg, s);
+            if (npl <= 1) return launch_geom_step<8, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_step<8, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_step<8, 4>(a, waves_per_wg, s);
+            return launch_geom_step<8, 8>(a, waves_per_wg, s);
         case 16:
-            if (npl <= 1) return launch_geom_xw<16, 1>(a, waves_per_wg, s);
-            if (npl <= 2) return launch_geom_xw<16, 2>(a, waves_per_wg, s);
-            if (npl <= 4) return launch_geom_xw<16, 4>(a, waves_per_wg, s);
-            return launch_geom_xw<16, 8>(a, waves_per_wg, s);
+            if (npl <= 1) return launch_geom_step<16, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_step<16, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_step<16, 4>(a, waves_per_wg, s);
+            return launch_geom_step<16, 8>(a, waves_per_wg, s);
         case 32:
-            if (npl <= 1) return launch_geom_xw<32, 1>(a, waves_per_wg, s);
-            if (npl <= 2) return launch_geom_xw<32, 2>(a, waves_per_wg, s);
-            if (npl <= 4) return launch_geom_xw<32, 4>(a, waves_per_wg, s);
-            return launch_geom_xw<32, 8>(a, waves_per_wg, s);
+            if (npl <= 1) return launch_geom_step<32, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_step<32, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_step<32, 4>(a, waves_per_wg, s);
+            return launch_geom_step<32, 8>(a, waves_per_wg, s);
         default:
-            if (npl <= 1) return launch_geom_xw<64, 1>(a, waves_per_wg, s);
-            if (npl <= 2) return launch_geom_xw<64, 2>(a, waves_per_wg, s);
-            if (npl <= 4) return launch_geom_xw<64, 4>(a, waves_per_wg, s);
-            return launch_geom_xw<64, 8>(a, waves_per_wg, s);
+            if (npl <= 1) return launch_geom_step<64, 1>(a, waves_per_wg, s);
+            if (npl <= 2) return launch_geom_step<64, 2>(a, waves_per_wg, s);
+            if (npl <= 4) return launch_geom_step<64, 4>(a, waves_per_wg, s);
+            return launch_geom_step<64, 8>(a, waves_per_wg, s);
     }
 }
 
 }  // namespace mh
-#endif  // MH_CHAIN_XW_TU
+#endif  // MH_CHAIN_STEP_TU

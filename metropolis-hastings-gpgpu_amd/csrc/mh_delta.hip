@@ -611,7 +611,7 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
 
 // ---- the kernel ---------------------------------------------------------------------------
 
-template <int L, bool XW>
+template <int L, bool XW, bool TRACK>
 __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / L;
@@ -799,9 +799,11 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         replay<L>(ch, n, nxt.nmx, cnt_cl, cnt_sa, r, gbase, sc);
         DSTAMP(5);
         // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
-        if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
-            best_total = sc[0];
-            if (live) save_best(ch, a.best + cidx * (int64_t)(F_COUNT * n), n, r, L);
+        if constexpr (TRACK) {
+            if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
+                best_total = sc[0];
+                if (live) save_best(ch, a.best + cidx * (int64_t)(F_COUNT * n), n, r, L);
+            }
         }
         if (accept(rng, sc[0], cur_total)) {
             cur_total = sc[0];
@@ -863,12 +865,13 @@ hipError_t launch_delta_l(const LaunchArgs& a, int waves_per_wg, hipStream_t str
     const int64_t chains_per_wg = (int64_t)waves_per_wg * G;
     const int64_t blocks = (a.n_chains + chains_per_wg - 1) / chains_per_wg;
     const size_t lds = (size_t)a.dlay.hdr + (size_t)waves_per_wg * G * a.dlay.stride;
-    if (a.rng == RNG_CURAND_XORWOW)
-        hipLaunchKernelGGL((mh_delta_kernel<L, true>), dim3((unsigned)blocks),
-                           dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
+    const dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_wg));
+    if (a.rng == RNG_CURAND_XORWOW)  // (tracking compiled in, switched at run time)
+        hipLaunchKernelGGL((mh_delta_kernel<L, true, true>), grid, block, lds, stream, a);
+    else if (a.track != TRACK_OFF)
+        hipLaunchKernelGGL((mh_delta_kernel<L, false, true>), grid, block, lds, stream, a);
     else
-        hipLaunchKernelGGL((mh_delta_kernel<L, false>), dim3((unsigned)blocks),
-                           dim3((unsigned)(64 * waves_per_wg)), lds, stream, a);
+        hipLaunchKernelGGL((mh_delta_kernel<L, false, false>), grid, block, lds, stream, a);
     return hipGetLastError();
 }
 

@@ -101,9 +101,8 @@ __device__ __forceinline__ bool best_improves(int track, float star, float best)
 // r, r+L, ... x, y, rotY come from LDS; z, rotX, rotZ live in HBM (`ch.zrr`) and are swapped
 // there only on accept, so a pending swap (aux->swap_a/b >= 0) is applied here as
 // commit_swap_zrr would: ka takes kb's values, kb takes ka's rounded to float.
-// Out of line: it runs only when a chain finds a new best, and keeps the hot loop's code small.
 template <class Ptrs>
-__device__ __attribute__((noinline)) void save_best(const Ptrs& ch, double* dst, int n, int r, int L) {
+__device__ __forceinline__ void save_best(const Ptrs& ch, double* dst, int n, int r, int L) {
     const int ka = ch.aux->swap_a, kb = ch.aux->swap_b;
     for (int i = r; i < n; i += L) {
         dst[F_X * n + i] = ch.X[i];

@@ -11,7 +11,7 @@
 
 namespace mh {
 
-enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3, OP_STEP_XW = 4 };
+enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3, OP_STEP_XW = 4, OP_STEP_T = 5 };
 
 // Which stream the chains draw from (mh_options.rng).
 enum RngKind { RNG_PHILOX = 0, RNG_CURAND_XORWOW = 1 };
@@ -49,6 +49,7 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
                           int64_t chain_offset, mh_summary* out, hipStream_t s);
 hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hipStream_t s);
 hipError_t launch_step_xw(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
+hipError_t launch_step_best(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
 hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
                       float* uni, float* nrm, hipStream_t s);
 hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,

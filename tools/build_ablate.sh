@@ -17,6 +17,6 @@ for M in "$@"; do
     *) DEF=-DMH_ABLATE=$M ;;
   esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
-    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_delta.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
+    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
 done
 wait
