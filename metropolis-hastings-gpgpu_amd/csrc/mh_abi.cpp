@@ -221,27 +221,28 @@ struct Geometry {
     mh::DeltaLds dlay;
 };
 
-// Incremental step kernel geometry: 32 lanes per chain (measured best at N = 64..256) and the
-// waves per workgroup that keep the most chains resident per CU (LDS and the kernel's ~166
-// VGPRs = 12 waves per CU bound it). It is the default step from N = 100 up (config 5's N = 256:
-// 1.24e7 vs 9.4e6 chain-steps/s; at N <= 64 the full-evaluation kernel is faster).
-// $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES / $MH_DELTA_WAVES pin a shape.
+// Incremental step kernel geometry: the (lanes per chain, waves per workgroup) shape that keeps
+// the most chains resident per CU, as the runtime's occupancy calculator counts them (registers,
+// LDS, waves); ties go to more waves, i.e. more lanes per chain (L = 64 holds the kernel at ~96
+// VGPRs; L < 64 needs ~166). It is the default step from N = 100 up (at N <= 64 the
+// full-evaluation kernel is faster). $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES /
+// $MH_DELTA_WAVES pin a shape.
 void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     g.dlay = mh::make_delta_layout(n, c, r);
     const char* e = getenv("MH_DELTA");
     g.delta = e && *e ? atoi(e) != 0 : n >= 100;
-    const int want_l = getenv("MH_DELTA_LANES") ? atoi(getenv("MH_DELTA_LANES")) : 32;
+    const int want_l = getenv("MH_DELTA_LANES") ? atoi(getenv("MH_DELTA_LANES")) : 0;
     const int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
-    const int lds_cu = 160 * 1024, waves_cu_max = 12;
     int best_chains = -1, best_waves = -1;
     g.dL = 0;
-    for (int L : {8, 16, 32}) {
+    for (int L : {8, 16, 32, 64}) {
         if (want_l && L != want_l) continue;
-        for (int w : {1, 2, 4}) {
+        for (int w = 1; w <= 8; ++w) {
             if (want_w && w != want_w) continue;
             const size_t b = mh::delta_lds_bytes(g.dlay, L, w);
             if (b > (size_t)max_lds) continue;
-            const int waves = std::min((int)(lds_cu / b) * w, waves_cu_max / w * w);
+            const int blocks = mh::delta_blocks_per_cu(L, w, b);
+            const int waves = blocks * w;
             const int chains = waves * (64 / L);
             if (chains > best_chains || (chains == best_chains && waves > best_waves)) {
                 best_chains = chains;
@@ -251,7 +252,7 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
             }
         }
     }
-    if (g.dL == 0) g.delta = false;  // does not fit: full evaluation
+    if (g.dL == 0 || best_chains <= 0) g.delta = false;  // does not fit: full evaluation
 }
 
 bool choose_geometry(int n, int c, int r, int device, Geometry& g) {

@@ -87,7 +87,7 @@ struct DeltaPtrs {
     float *LCL, *LSA;
     DeltaAux* aux;
     double* zrr;  // HBM: z, rotX, rotZ rows of this chain
-    int W, SW, cap_cl, cap_sa, NP;
+    int W, SW, cap_cl, cap_sa, NP, NR, DL;
 };
 
 // ---- per-object quantities --------------------------------------------------------------------
@@ -523,6 +523,21 @@ __device__ __forceinline__ void commit_swap_zrr(const DeltaPtrs& ch, int n) {
 // for the float accumulators. Every lane reads three streams of NP entries -- multiplier m,
 // double d, float f -- and adds v = m * d + f; the streams a sum does not use are ones or
 // zeros, and each sequence is zero past its end, so v is the reference's term exactly.
+// Sums list terms [from, to) of `fs` (the float list of lane k = 4 or 5) into the float
+// accumulator a, four at a time: the reference's float accumulator with float terms, so the
+// double-rounded add of the dense walk equals the plain fp32 add (53 >= 2 * 24 + 2 bits). The
+// entries up to round4(to) are zero (x + 0 == x).
+__device__ __forceinline__ float list_walk(const float* fs, int from, int to, float a) {
+    for (int l = from; l < to; l += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(fs + l);
+        a = a + q.x;
+        a = a + q.y;
+        a = a + q.z;
+        a = a + q.w;
+    }
+    return a;
+}
+
 template <int L>
 __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl, int cnt_sa,
                        int r, int gbase, float out[8]) {
@@ -531,6 +546,7 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
     const float* ms = ch.ONES;
     const double* ds = ch.ZERO;
     const float* fs = reinterpret_cast<const float*>(ch.ZERO);
+    int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
         ds = k == 0 ? ch.X : ch.Y;
@@ -544,15 +560,21 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
         fs = ch.LSA;
     } else if (k == 6) {
         ds = ch.RPW;
+        lim = ch.NR;
     } else if (k == 7) {
         ds = ch.RANG;
+        lim = ch.NR;
     }
     double accf = 0.0, accd = 0.0;  // float- and double-accumulated walks of the same terms
-    for (int l0 = 0; l0 < ch.NP; l0 += 4) {
+    for (int l0 = 0; l0 < ch.DL; l0 += 4) {
+        const bool in = l0 < lim;
+        const float* msl = in ? ms : ch.ONES;
+        const double* dsl = in ? ds : ch.ZERO;
+        const float* fsl = in ? fs : reinterpret_cast<const float*>(ch.ZERO);
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            v[u] = (double)ms[l0 + u] * ds[l0 + u] + (double)fs[l0 + u];
+            v[u] = (double)msl[l0 + u] * dsl[l0 + u] + (double)fsl[l0 + u];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];
@@ -563,25 +585,26 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
     // buffer, rare) further windows rebuilt in place.
     const int cnt = k == 4 ? cnt_cl : (k == 5 ? cnt_sa : 0);
     const int cap = k == 4 ? ch.cap_cl : ch.cap_sa;
-    const int tail = group_max<L>(min(cnt, cap));
-    for (int l = ch.NP; l < tail; ++l)
-        if (l < cnt && l < cap) accf = (double)(float)(accf + (double)fs[l]);
+    float af = (float)accf;
+    const int tail = (min(cnt, cap) + 3) & ~3;
+    if (tail > ch.NP) af = list_walk(fs, ch.NP, tail, af);
     for (int lo = ch.cap_cl; lo < cnt_cl; lo += ch.cap_cl) {
         wave_sync();
         build_cl_list<L>(ch, rm.c, r, lo);
+        const int m = min(ch.cap_cl, cnt_cl - lo);
+        for (int l = m + r; l < ((m + 3) & ~3); l += L) ch.LCL[l] = 0.0f;
         wave_sync();
-        if (k == 4)
-            for (int l = 0; l < ch.cap_cl && lo + l < cnt_cl; ++l)
-                accf = (double)(float)(accf + (double)ch.LCL[l]);
+        if (k == 4) af = list_walk(ch.LCL, 0, (m + 3) & ~3, af);
     }
     for (int lo = ch.cap_sa; lo < cnt_sa; lo += ch.cap_sa) {
         wave_sync();
         build_sa_list<L>(ch, n, rm.c, r, lo);
+        const int m = min(ch.cap_sa, cnt_sa - lo);
+        for (int l = m + r; l < ((m + 3) & ~3); l += L) ch.LSA[l] = 0.0f;
         wave_sync();
-        if (k == 5)
-            for (int l = 0; l < ch.cap_sa && lo + l < cnt_sa; ++l)
-                accf = (double)(float)(accf + (double)ch.LSA[l]);
+        if (k == 5) af = list_walk(ch.LSA, 0, (m + 3) & ~3, af);
     }
+    accf = (double)af;
     const bool acc_float = (k == 0 || k == 1 || k == 3 || k == 4 || k == 5);
     const double acc = acc_float ? accf : accd;
     const float nx = (float)grp_get<L>(acc, 0, gbase);
@@ -612,7 +635,9 @@ __device__ void replay(const DeltaPtrs& ch, int n, const float* nmx, int cnt_cl,
 // ---- the kernel ---------------------------------------------------------------------------
 
 template <int L, bool XW, bool TRACK>
-__global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
+// Up to 8 waves per workgroup: at large N one workgroup per CU holds every resident chain, so
+// the room tables staged in LDS are paid for once per CU.
+__global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / L;
     const DeltaLds& lay = a.dlay;
@@ -638,7 +663,7 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         float* area = reinterpret_cast<float*>(lds + lay.h_area);
         float* ones = reinterpret_cast<float*>(lds + lay.h_ones);
         double* zero = reinterpret_cast<double*>(lds + lay.h_zero);
-        for (int i = threadIdx.x; i < lay.NP; i += blockDim.x) {
+        for (int i = threadIdx.x; i < lay.DL; i += blockDim.x) {
             area[i] = i < n ? a.objc[i].area : 0.0f;
             ones[i] = 1.0f;
             zero[i] = 0.0;
@@ -683,9 +708,11 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
     ch.cap_cl = lay.cap_cl;
     ch.cap_sa = lay.cap_sa;
     ch.NP = np;
+    ch.NR = lay.NR;
+    ch.DL = lay.DL;
     const int64_t cidx = live ? chain : 0;
     ch.zrr = a.st + cidx * (int64_t)(F_COUNT * n) + F_Z * n;
-    const int nrp = (lay.RANG - lay.RPW) / 8;  // relationship stream length (>= NP)
+    const int nrp = lay.NR;  // relationship stream length
 
     // Stage the configuration, zero the streams past their ends, build every cache.
     const double* src = a.st + cidx * (int64_t)(F_COUNT * n);
@@ -783,8 +810,11 @@ __global__ void __launch_bounds__(256) mh_delta_kernel(LaunchArgs a) {
         DSTAMP(3);
         const int cnt_cl = build_cl_list<L>(ch, c, r, 0);
         const int cnt_sa = build_sa_list<L>(ch, n, c, r, 0);
-        for (int l = cnt_cl + r; l < np; l += L) ch.LCL[l] = 0.0f;  // zero past each list's end
-        for (int l = cnt_sa + r; l < np; l += L) ch.LSA[l] = 0.0f;
+        // zero past each list's end: to NP for the dense walk, to round4 for the list walk
+        const int zcl = max(np, (min(cnt_cl, ch.cap_cl) + 3) & ~3);
+        const int zsa = max(np, (min(cnt_sa, ch.cap_sa) + 3) & ~3);
+        for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) ch.LCL[l] = 0.0f;
+        for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) ch.LSA[l] = 0.0f;
         wave_sync();
         DSTAMP(4);
 #if MH_STAMPS > 1
@@ -892,12 +922,28 @@ size_t delta_lds_bytes(const DeltaLds& lay, int L, int waves_per_wg) {
     return (size_t)lay.hdr + (size_t)waves_per_wg * (64 / L) * lay.stride;
 }
 
+// Resident workgroups per CU of the plain step kernel for a shape (registers, LDS and the
+// wave limit all counted by the runtime). 0 if it does not fit.
+int delta_blocks_per_cu(int L, int waves_per_wg, size_t lds_bytes) {
+    int blocks = 0;
+    hipError_t e = hipErrorInvalidValue;
+    const int threads = 64 * waves_per_wg;
+    switch (L) {
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_delta_kernel<8, false, false>, threads, lds_bytes); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_delta_kernel<16, false, false>, threads, lds_bytes); break;
+        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_delta_kernel<32, false, false>, threads, lds_bytes); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_delta_kernel<64, false, false>, threads, lds_bytes); break;
+    }
+    return e == hipSuccess ? blocks : 0;
+}
+
 hipError_t launch_delta(const LaunchArgs& a, int L, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
     switch (L) {
         case 8: return launch_delta_l<8>(a, waves_per_wg, s);
         case 16: return launch_delta_l<16>(a, waves_per_wg, s);
-        default: return launch_delta_l<32>(a, waves_per_wg, s);
+        case 32: return launch_delta_l<32>(a, waves_per_wg, s);
+        default: return launch_delta_l<64>(a, waves_per_wg, s);
     }
 }
 

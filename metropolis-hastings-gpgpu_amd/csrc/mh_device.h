@@ -176,8 +176,10 @@ inline MH_HD int bank_place(int o, unsigned* used) {
 // stream of NP = round4(N + 1) entries, zero past its end (sentinels / zero fill).
 struct DeltaLds {
     int hdr, h_obj, h_clr, h_rel, h_frz, h_room;
-    int h_area, h_ones, h_zero;  // float[NP] areas, float[NP] ones, double[NP] zeros
+    int h_area, h_ones, h_zero;  // float[DL] areas, float[DL] ones, double[DL] zeros
     int NP;
+    int NR;         // relationship stream length round4(max(R, 1))
+    int DL;         // dense replay length max(NP, NR)
     int X, Y;       // double[NP] (zero past N)
     int RY;         // double[N]
     int P;          // float4[N] {xf, yf, rotYf, 0}
@@ -186,8 +188,9 @@ struct DeltaLds {
     int CLA;        // float4[C] clearance boxes at their source objects
     int NZ;         // uint64[C][W] non-zero Clearance pairs (row = clearance, bit = object)
     int SAM, SAMB;  // uint32[SW] non-zero SurfaceArea entries (C clearances then N objects), backup
-    int RPW, RANG;  // double[max(R, NP)] negated PairWise / PairWiseAngle terms (zero past R)
-    int LCL, LSA;   // float[cap] compacted negated Clearance / SurfaceArea terms (zero filled)
+    int RPW, RANG;  // double[NR] negated PairWise / PairWiseAngle terms (zero past R)
+    int LCL, LSA;   // float[cap] compacted negated Clearance / SurfaceArea terms (zero filled
+                    // to max(NP, round4(count)))
     int AUX;        // per-chain scalars (backups, current costs)
     int W, SW;      // words per NZ row, SAM words
     int cap_cl, cap_sa;
@@ -202,15 +205,19 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     const int np = (n + 1 + 3) & ~3;
     l.NP = np;
     int h = room_header(n, c, r, l.h_obj, l.h_clr, l.h_rel, l.h_frz, l.h_room);
-    l.h_area = h; h += round16(4 * np);
-    l.h_ones = h; h += round16(4 * np);
-    l.h_zero = h; h += round16(8 * np);
+    l.NR = ((r > 1 ? r : 1) + 3) & ~3;
+    l.DL = np > l.NR ? np : l.NR;
+    l.h_area = h; h += round16(4 * l.DL);
+    l.h_ones = h; h += round16(4 * l.DL);
+    l.h_zero = h; h += round16(8 * l.DL);
     l.hdr = h;
     l.W = (n + 63) / 64;
     l.SW = (c + n + 31) / 32;
-    l.cap_cl = 2 * np < 32 ? 32 : 2 * np;
+    // Clearance list capacity: the non-zero pairs of a sampled room run to ~4 per object at
+    // N = 128..256 (tools/stamps.py counts build); longer lists are summed in windows.
+    l.cap_cl = 4 * np < 32 ? 32 : 4 * np;
     l.cap_sa = np < 32 ? 32 : np;
-    const int nrp = r > np ? ((r + 3) & ~3) : np;
+    const int nrp = l.NR;
     int o = 0;
     l.X = o;    o += 8 * np;
     l.Y = o;    o += 8 * np;

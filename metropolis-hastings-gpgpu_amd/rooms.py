@@ -90,15 +90,17 @@ class SplitMix64:
         return self.next() % k
 
 
-def synthetic_room(n: int, freeze_every: int = 0, seed: int | None = None) -> Room:
+def synthetic_room(n: int, freeze_every: int = 0, seed: int | None = None,
+                   n_rel: int | None = None) -> Room:
     """SURVEY.md 8(d) synthetic room. Draw order: per clearance (a, b, source); per object
-    (a, b, x, y, rotY); per relationship (source, target != source)."""
+    (a, b, x, y, rotY); per relationship (source, target != source). `n_rel` overrides the
+    N/2 relationships (test rooms with more relationships than objects)."""
     if n < 1:
         raise ValueError("n >= 1")
     rng = SplitMix64(0x5EED0000 + n if seed is None else seed)
     w = 2.5 * math.sqrt(n)
     ncl = n // 4
-    nrel = n // 2 if n >= 2 else 0
+    nrel = (n // 2 if n >= 2 else 0) if n_rel is None else (n_rel if n >= 2 else 0)
     srf = Surface()
     srf.nObjs, srf.nRelationships, srf.nClearances = n, nrel, ncl
     srf.WeightFocalPoint = 2.0

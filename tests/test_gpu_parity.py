@@ -24,6 +24,8 @@ def _room(mh, kind: str, n: int):
         return mh.main_fixture()
     if kind == "frozen":
         return mh.synthetic_room(n, freeze_every=4)
+    if kind == "manyrel":  # more relationships than objects: R > N + 1
+        return mh.synthetic_room(n, n_rel=3 * n + 5)
     room = mh.synthetic_room(n)
     if kind == "wrap":  # angle ranges crossing zero: the fmodf branch of Kernel.cu:245-250
         for k in range(room.srf.nRelationships):
@@ -146,6 +148,8 @@ def test_chains_match_oracle(mh, orc, hiplib, kind, n, chains, steps):
     ("syn", 9, 128, 500),
     ("syn", 64, 64, 600),
     ("syn", 100, 16, 120),
+    ("manyrel", 8, 64, 300),
+    ("manyrel", 100, 16, 100),
 ])
 def test_chains_match_oracle_each_step_kernel(mh, orc, hiplib, monkeypatch, step, kind, n,
                                               chains, steps):
