@@ -224,13 +224,14 @@ struct Geometry {
 // Incremental step kernel geometry: the (lanes per chain, waves per workgroup) shape that keeps
 // the most chains resident per CU, as the runtime's occupancy calculator counts them (registers,
 // LDS, waves); ties go to more waves, i.e. more lanes per chain (L = 64 holds the kernel at ~96
-// VGPRs; L < 64 needs ~166). It is the default step from N = 100 up (at N <= 64 the
-// full-evaluation kernel is faster). $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES /
+// VGPRs; L < 64 needs ~166). It is the default step above N = 128 (measured, chain-steps/s
+// full vs incremental: N = 100 1.21e8 / 1.15e8, N = 128 8.8e7 / 8.8e7, N = 192 2.0e7 / 5.0e7,
+// N = 256 8.9e6 / 3.1e7). $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES /
 // $MH_DELTA_WAVES pin a shape.
 void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     g.dlay = mh::make_delta_layout(n, c, r);
     const char* e = getenv("MH_DELTA");
-    g.delta = e && *e ? atoi(e) != 0 : n >= 100;
+    g.delta = e && *e ? atoi(e) != 0 : n > 128;
     const int want_l = getenv("MH_DELTA_LANES") ? atoi(getenv("MH_DELTA_LANES")) : 0;
     const int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
     int best_chains = -1, best_waves = -1;

@@ -482,3 +482,29 @@ def test_xorwow_sharded_sessions_equal_one(mh, hiplib):
                           p_all.view(np.uint32))
     assert np.array_equal(np.concatenate([p[1] for p in parts]).view(np.uint32),
                           c_all.view(np.uint32))
+
+
+# ---- size limits ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("n", [511, 512])
+def test_maximum_room_size(mh, orc, hiplib, monkeypatch, step, n):
+    """The largest rooms the library accepts (64 lanes x 8 objects per lane = 512): both step
+    kernels against the oracle, bit for bit."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    room = mh.synthetic_room(n)
+    chains, steps, seed = 8, 30, 512
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
+    assert np.array_equal(pts.view(np.uint32), ref_pts.view(np.uint32))
+    assert np.array_equal(costs.view(np.uint32), ref_costs.view(np.uint32))
+
+
+def test_oversized_room_is_rejected(mh, hiplib):
+    room = mh.synthetic_room(513)
+    with pytest.raises(mh.MHError, match="too large"):
+        mh.kernel_wrapper(room, 4, 10, seed=1)
