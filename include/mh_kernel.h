@@ -165,17 +165,29 @@ typedef enum mh_rng_kind {
 } mh_rng_kind;
 
 typedef struct mh_options {
-    uint64_t seed;       /* RNG seed (see mh_rng_kind) */
-    int32_t track_best;  /* mh_track_best. The initial configuration is the first best; every
-                            proposal (accepted or not) is compared before the accept test; ties
-                            keep the earlier one. */
-    int32_t rng;         /* mh_rng_kind */
-    int32_t reserved[4]; /* must be zero */
+    uint64_t seed;         /* RNG seed (see mh_rng_kind) */
+    int32_t track_best;    /* mh_track_best. The initial configuration is the first best; every
+                              proposal (accepted or not) is compared before the accept test; ties
+                              keep the earlier one. */
+    int32_t rng;           /* mh_rng_kind */
+    int32_t n_temps;       /* parallel tempering: replicas per group (0 or 1 = off). Chains
+                              [g*K, (g+1)*K) form group g; chain g*K+k starts at rung k, whose
+                              inverse temperature is beta_k = 2 * (beta_min / 2)^(k / (K-1)):
+                              rung 0 is the reference's BETA = 2 (Kernel.cu:706-713). The chain
+                              count must be a multiple of K. */
+    int32_t swap_interval; /* MH steps between replica-exchange rounds (>= 1 with tempering) */
+    double beta_min;       /* inverse temperature of the hottest rung, 0 < beta_min <= 2 */
+    int32_t reserved[4];   /* must be zero */
 } mh_options;
 
 /* KernelWrapper with options (NULL = KernelWrapper's defaults with seed $MH_SEED/time). With
  * track_best != MH_TRACK_OFF, result[i] holds chain i's best configuration and its eight cost
- * components (OffLimits included, as bestCosts would hold them). */
+ * components (OffLimits included, as bestCosts would hold them). With parallel tempering,
+ * result[g*K + k] holds the replica that ends at rung k of group g, so result[g*K] are the
+ * BETA = 2 samples. Exchange round t (after steps t*swap_interval, t = 1, 2, ...) tries the
+ * rung pairs (k, k+1) with k = (t-1) mod 2, 2 + (t-1) mod 2, ...; the pair swaps rungs when
+ * u < min(1, (float)exp((beta_k - beta_k+1) * (E_k+1 - E_k))), E = current totalCosts, u the
+ * Philox uniform of (key = seed, subsequence = 2^63 + g, offset = (t-1)*K + k). */
 MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct* rsa,
                                positionAndRotation* cfg, rectangle* clearances,
                                rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
@@ -310,6 +322,7 @@ MH_STATIC_ASSERT(sizeof(resultCosts) == 32, "resultCosts");
 MH_STATIC_ASSERT(sizeof(result) == 40, "result");
 MH_STATIC_ASSERT(offsetof(result, costs) == 8, "result.costs");
 MH_STATIC_ASSERT(sizeof(mh_summary) == 40, "mh_summary");
-MH_STATIC_ASSERT(sizeof(mh_options) == 32, "mh_options");
+MH_STATIC_ASSERT(sizeof(mh_options) == 48, "mh_options");
+MH_STATIC_ASSERT(offsetof(mh_options, beta_min) == 24, "mh_options.beta_min");
 
 #endif /* MH_KERNEL_H_ */

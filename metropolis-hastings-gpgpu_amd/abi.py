@@ -86,7 +86,13 @@ class mh_summary(C.Structure):
 
 class mh_options(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("rng", C.c_int32),
+                ("n_temps", C.c_int32), ("swap_interval", C.c_int32), ("beta_min", C.c_double),
                 ("reserved", C.c_int32 * 4)]
+
+
+def options(seed: int, track: int = 0, rng: int = 0, temps: int = 1, swap_interval: int = 1,
+            beta_min: float = 2.0) -> "mh_options":
+    return mh_options(seed, track, rng, temps, swap_interval, beta_min)
 
 
 MH_TRACK_OFF, MH_TRACK_LOWEST, MH_TRACK_HIGHEST = 0, 1, 2
@@ -106,7 +112,8 @@ STRUCT_LAYOUT = {  # (size, {field: offset}) as static_assert-ed in include/mh_k
     resultCosts: (32, {}),
     result: (40, {"costs": 8}),
     mh_summary: (40, {}),
-    mh_options: (32, {"track_best": 8, "rng": 12}),
+    mh_options: (48, {"track_best": 8, "rng": 12, "n_temps": 16, "swap_interval": 20,
+                      "beta_min": 24}),
 }
 
 COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointCosts",
@@ -237,16 +244,18 @@ def points_to_array(pts, count: int) -> np.ndarray:
 # ---- calls -----------------------------------------------------------------------------------
 
 def kernel_wrapper(room: Room, chains: int, iterations: int, seed: int | None = None,
-                   block_x: int = 64, track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX):
+                   block_x: int = 64, track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX,
+                   temps: int = 1, swap_interval: int = 1, beta_min: float = 2.0):
     """Calls KernelWrapper (or KernelWrapperSeeded, or KernelWrapperEx when `track` or `rng`
     is set) exactly as the reference's caller does and returns (points [chains, N, 6] float32,
     costs [chains, 8] float32)."""
     lib = load_library()
     g = gpuConfig(chains, 0, block_x, 0, 0, iterations)
-    if track or rng:
+    if track or rng or temps > 1:
         if seed is None:
             raise ValueError("KernelWrapperEx needs an explicit seed")
-        res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh_options(seed, track, rng)))
+        opts = options(seed, track, rng, temps, swap_interval, beta_min)
+        res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(opts))
     elif seed is None:
         res = lib.KernelWrapper(*room.args(), C.byref(g))
     else:
@@ -312,14 +321,16 @@ class Session:
     """Device-resident chains: the shard one rank owns (chain ids [offset, offset + chains))."""
 
     def __init__(self, room: Room, chains: int, seed: int, device: int = 0, chain_offset: int = 0,
-                 track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX):
+                 track: int = MH_TRACK_OFF, rng: int = MH_RNG_PHILOX, temps: int = 1,
+                 swap_interval: int = 1, beta_min: float = 2.0):
         self.lib = load_library()
         self.room = room
         self.chains = chains
         self.chain_offset = chain_offset
-        if track or rng:
+        if track or rng or temps > 1:
+            opts = options(seed, track, rng, temps, swap_interval, beta_min)
             h = self.lib.mh_session_create_ex(*room.args(), device, chains, chain_offset,
-                                              C.byref(mh_options(seed, track, rng)))
+                                              C.byref(opts))
         else:
             h = self.lib.mh_session_create(*room.args(), device, chains, chain_offset,
                                            C.c_uint64(seed))

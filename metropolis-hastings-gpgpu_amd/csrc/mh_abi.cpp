@@ -281,6 +281,18 @@ bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     return true;
 }
 
+// The options every entry point resolves to (mh_options with defaults applied).
+mh_options default_options(uint64_t seed) {
+    mh_options o{};
+    o.seed = seed;
+    o.track_best = MH_TRACK_OFF;
+    o.rng = MH_RNG_PHILOX;
+    o.n_temps = 1;
+    o.swap_interval = 1;
+    o.beta_min = mh::kBeta;
+    return o;
+}
+
 bool check_options(const mh_options* o) {
     if (o->track_best < MH_TRACK_OFF || o->track_best > MH_TRACK_HIGHEST) {
         set_error("mh_options.track_best must be MH_TRACK_OFF, MH_TRACK_LOWEST or MH_TRACK_HIGHEST");
@@ -288,6 +300,15 @@ bool check_options(const mh_options* o) {
     }
     if (o->rng < MH_RNG_PHILOX || o->rng > MH_RNG_CURAND_XORWOW) {
         set_error("mh_options.rng must be MH_RNG_PHILOX or MH_RNG_CURAND_XORWOW");
+        return false;
+    }
+    if (o->n_temps < 0 || o->n_temps > 1024) {
+        set_error("mh_options.n_temps must be in [0, 1024]");
+        return false;
+    }
+    if (o->n_temps > 1 && (o->swap_interval < 1 || !(o->beta_min > 0.0) ||
+                           !(o->beta_min <= mh::kBeta))) {
+        set_error("parallel tempering needs swap_interval >= 1 and 0 < beta_min <= 2");
         return false;
     }
     for (int k = 0; k < 4; ++k)
@@ -316,6 +337,12 @@ struct mh_session {
     int track = mh::TRACK_OFF;
     int rng = mh::RNG_PHILOX;
     unsigned int* d_xw = nullptr;  // [n_chains][6] XORWOW states (rng == RNG_CURAND_XORWOW)
+    int n_temps = 1;               // parallel tempering replicas per group
+    int swap_interval = 1;
+    int64_t steps_done = 0;        // MH steps run so far (exchange rounds fall on multiples)
+    std::vector<double> ladder;    // [n_temps] inverse temperatures, ladder[0] = BETA
+    double* d_ladder = nullptr;
+    int* d_perm = nullptr;         // [n_chains] rung -> group-local chain (per group)
     mh::ObjConst* d_obj = nullptr;
     mh::ClrConst* d_clr = nullptr;
     mh::RelConst* d_rel = nullptr;
@@ -346,6 +373,8 @@ struct mh_session {
         a.best = d_best;
         a.rng = rng;
         a.xw = d_xw;
+        a.n_temps = n_temps;
+        a.ladder = d_ladder;
         a.lay = geo.lay;
         a.dlay = geo.dlay;
         return a;
@@ -367,6 +396,8 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_st);
     (void)hipFree(s->d_best);
     (void)hipFree(s->d_xw);
+    (void)hipFree(s->d_ladder);
+    (void)hipFree(s->d_perm);
     (void)hipFree(s->d_meta);
     (void)hipFree(s->d_pts);
     (void)hipFree(s->d_costs);
@@ -396,6 +427,15 @@ bool session_init(mh_session* s) {
     MH_TRY_HIP(hipMalloc((void**)&s->d_st, sizeof(double) * mh::F_COUNT * n * nc));
     if (s->track != mh::TRACK_OFF)
         MH_TRY_HIP(hipMalloc((void**)&s->d_best, sizeof(double) * mh::F_COUNT * n * nc));
+    if (s->n_temps > 1) {
+        MH_TRY_HIP(hipMalloc((void**)&s->d_ladder, sizeof(double) * s->n_temps));
+        MH_TRY_HIP(hipMemcpyAsync(s->d_ladder, s->ladder.data(), sizeof(double) * s->n_temps,
+                                  hipMemcpyHostToDevice, s->stream));
+        std::vector<int> perm((size_t)nc);
+        for (int64_t i = 0; i < (int64_t)perm.size(); ++i) perm[(size_t)i] = (int)(i % s->n_temps);
+        MH_TRY_HIP(hipMalloc((void**)&s->d_perm, sizeof(int) * perm.size()));
+        MH_TRY_HIP(hipMemcpy(s->d_perm, perm.data(), sizeof(int) * perm.size(), hipMemcpyHostToDevice));
+    }
     if (s->rng == mh::RNG_CURAND_XORWOW) {
         MH_TRY_HIP(hipMalloc((void**)&s->d_xw, sizeof(unsigned int) * 6 * nc));
         MH_TRY_HIP(mh::launch_xorwow_init(s->seed, s->chain_offset, s->n_chains, s->d_xw, s->stream));
@@ -423,10 +463,17 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
         MH_TRY_HIP(hipEventDestroy(ev));
     }
     mh::LaunchArgs a = s->args();
-    for (int done = 0; done < iterations; done += kStepsPerLaunch) {
-        a.iterations = std::min(kStepsPerLaunch, iterations - done);
+    for (int done = 0; done < iterations;) {
+        int chunk = std::min(kStepsPerLaunch, iterations - done);
+        if (s->n_temps > 1)  // stop at the next exchange round
+            chunk = (int)std::min<int64_t>(chunk, s->swap_interval - s->steps_done % s->swap_interval);
+        a.iterations = chunk;
         if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dL, s->geo.dwaves, st));
         else MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
+        done += chunk;
+        s->steps_done += chunk;
+        if (s->n_temps > 1 && s->steps_done % s->swap_interval == 0)
+            MH_TRY_HIP(mh::launch_exchange(a, s->d_perm, (int)(s->steps_done / s->swap_interval), st));
     }
     return true;
 }
@@ -452,10 +499,22 @@ bool session_download(mh_session* s, point* pts, resultCosts* costs) {
 }
 
 mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
-                           uint64_t seed, int track, int rng = mh::RNG_PHILOX) {
+                           const mh_options& o) {
+    const int K = o.n_temps > 1 ? o.n_temps : 1;
+    if (K > 1 && (n_chains % K != 0 || chain_offset % K != 0)) {
+        set_error("parallel tempering: the chain count and offset must be multiples of n_temps");
+        return nullptr;
+    }
+    const uint64_t seed = o.seed;
     mh_session* s = new mh_session();
-    s->track = track;
-    s->rng = rng;
+    s->track = o.track_best;
+    s->rng = o.rng;
+    s->n_temps = K;
+    s->swap_interval = o.swap_interval > 0 ? o.swap_interval : 1;
+    s->ladder.resize((size_t)K);
+    for (int k = 0; k < K; ++k)  // geometric from BETA (rung 0) down to beta_min
+        s->ladder[(size_t)k] = k == 0 ? mh::kBeta
+                                      : mh::kBeta * pow(o.beta_min / mh::kBeta, (double)k / (K - 1));
     s->device = device;
     s->room = room;
     s->n_chains = n_chains;
@@ -508,8 +567,8 @@ struct Shard {
 
 result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, positionAndRotation* cfg,
                      rectangle* clearances, rectangle* offlimits, vertex* vertices,
-                     vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg, uint64_t seed,
-                     int track, int rng = mh::RNG_PHILOX) {
+                     vertex* surfaceRectangle, Surface* srf, gpuConfig* gpuCfg,
+                     const mh_options& opts) {
     if (!gpuCfg) { set_error("gpuCfg is NULL"); return nullptr; }
     if (gpuCfg->gridxDim < 1) { set_error("gpuConfig.gridxDim must be >= 1"); return nullptr; }
     if (gpuCfg->iterations < 0) { set_error("gpuConfig.iterations must be >= 0"); return nullptr; }
@@ -536,14 +595,24 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         set_error("host allocation failed");
         return nullptr;
     }
+    // Shard whole tempering groups (K = 1 without tempering).
+    const int64_t K = opts.n_temps > 1 ? opts.n_temps : 1;
+    if (chains % K != 0) {
+        free(pts);
+        free(res);
+        set_error("parallel tempering: gridxDim must be a multiple of n_temps");
+        return nullptr;
+    }
+    const int64_t groups = chains / K;
+    if ((int64_t)devs.size() > groups) devs.resize((size_t)groups);
     std::vector<Shard> shards(devs.size());
     for (size_t k = 0; k < devs.size(); ++k) {
         shards[k].device = devs[k];
-        shards[k].begin = chains * (int64_t)k / (int64_t)devs.size();
-        shards[k].count = chains * (int64_t)(k + 1) / (int64_t)devs.size() - shards[k].begin;
+        shards[k].begin = K * (groups * (int64_t)k / (int64_t)devs.size());
+        shards[k].count = K * (groups * (int64_t)(k + 1) / (int64_t)devs.size()) - shards[k].begin;
     }
     auto work = [&](Shard& sh) {
-        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, seed, track, rng);
+        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, opts);
         if (!s) {
             sh.err = g_last_error;
             return;
@@ -586,7 +655,7 @@ MH_API result* KernelWrapper(relationshipStruct* rss, relationshipAngleStruct* r
                              vertex* vertices, vertex* surfaceRectangle, Surface* srf,
                              gpuConfig* gpuCfg) {
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, seed_from_env(), mh::TRACK_OFF);
+                        gpuCfg, default_options(seed_from_env()));
 }
 
 MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStruct* rsa,
@@ -594,7 +663,7 @@ MH_API result* KernelWrapperSeeded(relationshipStruct* rss, relationshipAngleStr
                                    rectangle* offlimits, vertex* vertices, vertex* surfaceRectangle,
                                    Surface* srf, gpuConfig* gpuCfg, uint64_t seed) {
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, seed, mh::TRACK_OFF);
+                        gpuCfg, default_options(seed));
 }
 
 MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct* rsa,
@@ -603,10 +672,10 @@ MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct*
                                Surface* srf, gpuConfig* gpuCfg, const mh_options* opts) {
     if (!opts)
         return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle,
-                            srf, gpuCfg, seed_from_env(), mh::TRACK_OFF);
+                            srf, gpuCfg, default_options(seed_from_env()));
     if (!check_options(opts)) return nullptr;
     return wrapper_impl(rss, rsa, cfg, clearances, offlimits, vertices, surfaceRectangle, srf,
-                        gpuCfg, opts->seed, opts->track_best, opts->rng);
+                        gpuCfg, *opts);
 }
 
 MH_API void KernelFreeResult(result* res) {
@@ -643,7 +712,7 @@ MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationship
     }
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) { set_error("no HIP device available"); return -1; }
-    mh_session* s = session_create(room, device, 0, 0, 0, mh::TRACK_OFF);  // tables only
+    mh_session* s = session_create(room, device, 0, 0, default_options(0));  // tables only
     if (!s) return -1;
     bool ok = true;
     double* d_cfgs = nullptr;
@@ -689,7 +758,7 @@ MH_API mh_session* mh_session_create(const relationshipStruct* rss,
         set_error("invalid HIP device " + std::to_string(device));
         return nullptr;
     }
-    return session_create(room, device, n_chains, chain_offset, seed, mh::TRACK_OFF);
+    return session_create(room, device, n_chains, chain_offset, default_options(seed));
 }
 
 MH_API mh_session* mh_session_create_ex(const relationshipStruct* rss,
@@ -710,8 +779,7 @@ MH_API mh_session* mh_session_create_ex(const relationshipStruct* rss,
         set_error("invalid HIP device " + std::to_string(device));
         return nullptr;
     }
-    return session_create(room, device, n_chains, chain_offset, opts->seed, opts->track_best,
-                          opts->rng);
+    return session_create(room, device, n_chains, chain_offset, *opts);
 }
 
 MH_API int mh_session_run(mh_session* s, int iterations, void* stream) {

@@ -823,6 +823,13 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch) {
 #define MH_OCC
 #endif
 
+// Output slot of a chain: with parallel tempering the replica at rung k of group g goes to
+// g*K + k (a session's chain offset and count are multiples of K).
+__device__ __forceinline__ int64_t out_index(const LaunchArgs& a, int64_t chain) {
+    if (a.n_temps <= 1) return chain;
+    return chain - chain % a.n_temps + a.meta[chain].rung;
+}
+
 template <int L, int NPL, int OP>
 __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -928,7 +935,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             m.bm_val = 0.0f;
             for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
             m.best_total = cur[0];  // cfgBest := the initial configuration, Kernel.cu:779-782
-            m.pad = 0;
+            m.rung = a.n_temps > 1 ? (int)((a.chain_offset + chain) % a.n_temps) : 0;
             a.meta[chain] = m;
         }
     } else if constexpr (STEP) {
@@ -941,6 +948,9 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         rng_load(rng, a, chain, m0);
         uint64_t accepted = m0.accepted;
         float best_total = m0.best_total;
+        double beta = kBeta;
+        if constexpr (TRACK)  // (the extended families also carry parallel tempering)
+            if (a.n_temps > 1) beta = a.ladder[m0.rung];
         eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
 #if MH_STAMPS
         if (writer)
@@ -964,7 +974,10 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
                     save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
                 }
             }
-            if (accept(rng, sc[0], cur_total)) {
+            bool acc;
+            if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
+            else acc = accept(rng, sc[0], cur_total);
+            if (acc) {
                 cur_total = sc[0];
                 sym = ss;
                 ++accepted;
@@ -991,7 +1004,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             rng_save(rng, a, chain);
             for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
             m.best_total = best_total;
-            m.pad = 0;
+            m.rung = m0.rung;
             a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
@@ -1006,7 +1019,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             rc.ClearanceCosts = cur[5];
             rc.OffLimitsCosts = cur[6];
             rc.SurfaceAreaCosts = cur[7];
-            a.costs[chain] = rc;
+            a.costs[out_index(a, chain)] = rc;
         }
         if constexpr (OP == OP_FINAL) {
             for (int i = r; i < n; i += L) {
@@ -1017,7 +1030,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
                 p.rotX = (float)ch.zrr[n + i];
                 p.rotY = (float)ch.RY[i];
                 p.rotZ = (float)ch.zrr[2 * n + i];
-                a.pts[chain * (int64_t)n + i] = p;
+                a.pts[out_index(a, chain) * (int64_t)n + i] = p;
             }
         }
     }
@@ -1171,6 +1184,36 @@ __global__ void mh_rng_xw_kernel(uint64_t seed, uint64_t subsequence, int n, uns
     }
 }
 
+// ---- parallel tempering: one replica-exchange round ----------------------------------------
+
+// One thread per group of K = n_temps chains. perm[g*K + k] is the group-local index of the
+// chain at rung k. Round t tries the disjoint rung pairs (k, k+1), k = (t-1) mod 2 + 2i, with
+// the Philox uniform (key = seed, subsequence = 2^63 + global group, offset = (t-1)*K + k) and
+// the exchange rule for pi_beta ~ exp(beta * totalCosts) (the maximisation Accept performs).
+__global__ void __launch_bounds__(256) mh_exchange_kernel(LaunchArgs a, int* perm, int round) {
+    const int K = a.n_temps;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g * K >= a.n_chains) return;
+    int* pg = perm + g * K;
+    ChainMeta* mg = a.meta + g * K;
+    const uint64_t gid = (uint64_t)(a.chain_offset / K + g);
+    for (int k = (round - 1) & 1; k + 1 < K; k += 2) {
+        const int ca = pg[k], cb = pg[k + 1];
+        const float ea = mg[ca].costs[0], eb = mg[cb].costs[0];
+        rocrand_state_philox4x32_10 st;
+        rocrand_init(a.seed, (1ull << 63) | gid, (uint64_t)(round - 1) * K + k, &st);
+        const float u = rocrand_device::detail::uniform_distribution(rocrand(&st));
+        const double db = a.ladder[k] - a.ladder[k + 1];
+        const float thr = fminf(1.0f, (float)exp(db * ((double)eb - (double)ea)));
+        if (u < thr) {
+            pg[k] = cb;
+            pg[k + 1] = ca;
+            mg[ca].rung = k + 1;
+            mg[cb].rung = k;
+        }
+    }
+}
+
 // ---- diagnostic: the group collectives on given lane values ---------------------------------
 
 // out[k * 64 + lane] for k = 0 top-2 m1, 1 m2, 2 argmax (lane index within the group, values
@@ -1244,7 +1287,8 @@ size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
     if (op == OP_STEP && a.rng == RNG_CURAND_XORWOW) return launch_step_xw(a, L, npl, waves_per_wg, s);
-    if (op == OP_STEP && a.track != TRACK_OFF) return launch_step_best(a, L, npl, waves_per_wg, s);
+    if (op == OP_STEP && (a.track != TRACK_OFF || a.n_temps > 1))
+        return launch_step_best(a, L, npl, waves_per_wg, s);
     // (lanes per chain, objects per lane) instantiations; npl rounds up to the next one.
     switch (L) {
         case 8:
@@ -1300,6 +1344,14 @@ hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsi
         hipLaunchKernelGGL(mh_rng_xw_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
     else
         hipLaunchKernelGGL(mh_rng_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+    return hipGetLastError();
+}
+
+hipError_t launch_exchange(const LaunchArgs& a, int* perm, int round, hipStream_t s) {
+    const int64_t groups = a.n_chains / a.n_temps;
+    if (groups <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mh_exchange_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s,
+                       a, perm, round);
     return hipGetLastError();
 }
 

@@ -542,4 +542,12 @@ __device__ __forceinline__ bool accept(Rng& rng, float star, float cur) {
     return u < thr;
 }
 
+// The same at inverse temperature beta (parallel tempering; beta = kBeta is Accept itself).
+template <class Rng>
+__device__ __forceinline__ bool accept_at(Rng& rng, float star, float cur, double beta) {
+    const float u = rng.uniform();
+    const float thr = fminf(1.0f, (float)exp(beta * ((double)star - (double)cur)));
+    return u < thr;
+}
+
 }  // namespace mh

@@ -769,6 +769,9 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     rng_load(rng, a, cidx, m0);
     uint64_t accepted = m0.accepted;
     float best_total = m0.best_total;
+    double beta = kBeta;
+    if constexpr (TRACK)  // (the extended variants also carry parallel tempering)
+        if (a.n_temps > 1) beta = a.ladder[m0.rung];
     int rc = 0;  // which RM buffer holds the current rows
 #if MH_STAMPS
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last;
@@ -835,7 +838,10 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
                 if (live) save_best(ch, a.best + cidx * (int64_t)(F_COUNT * n), n, r, L);
             }
         }
-        if (accept(rng, sc[0], cur_total)) {
+        bool acc;
+        if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
+        else acc = accept(rng, sc[0], cur_total);
+        if (acc) {
             cur_total = sc[0];
             ++accepted;
             rc ^= 1;
@@ -876,7 +882,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
         rng_save(rng, a, chain);
         for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
         m.best_total = best_total;
-        m.pad = 0;
+        m.rung = m0.rung;
         a.meta[chain] = m;
     }
     if (live) {
@@ -898,7 +904,7 @@ hipError_t launch_delta_l(const LaunchArgs& a, int waves_per_wg, hipStream_t str
     const dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_wg));
     if (a.rng == RNG_CURAND_XORWOW)  // (tracking compiled in, switched at run time)
         hipLaunchKernelGGL((mh_delta_kernel<L, true, true>), grid, block, lds, stream, a);
-    else if (a.track != TRACK_OFF)
+    else if (a.track != TRACK_OFF || a.n_temps > 1)
         hipLaunchKernelGGL((mh_delta_kernel<L, false, true>), grid, block, lds, stream, a);
     else
         hipLaunchKernelGGL((mh_delta_kernel<L, false, false>), grid, block, lds, stream, a);

@@ -78,7 +78,7 @@ struct ChainMeta {
     float bm_val;       // cached second normal
     float costs[8];     // resultCosts of the current state
     float best_total;   // best-of-chain tracking: totalCosts of the saved best configuration
-    int pad;
+    int rung;           // parallel tempering: this chain's temperature index (0 = BETA)
 };
 static_assert(sizeof(ChainMeta) == 64, "ChainMeta");
 

@@ -33,6 +33,8 @@ struct LaunchArgs {
     int track;               // TRACK_OFF / TRACK_LOWEST / TRACK_HIGHEST
     double* best;            // [n_chains][6][N] best-of-chain configurations (track != 0)
     int rng;                 // RngKind
+    int n_temps;             // parallel tempering replicas per group (1 = off)
+    const double* ladder;    // [n_temps] inverse temperatures (n_temps > 1)
     unsigned int* xw;        // [n_chains][6] XORWOW states {d, x0..x4} (rng == RNG_CURAND_XORWOW)
     ChainLds lay;
     DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
@@ -53,6 +55,7 @@ hipError_t launch_step_xw(const LaunchArgs& a, int L, int npl, int waves_per_wg,
 hipError_t launch_step_best(const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s);
 hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
                       float* uni, float* nrm, hipStream_t s);
+hipError_t launch_exchange(const LaunchArgs& a, int* perm, int round, hipStream_t s);
 hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
                               hipStream_t s);
 

@@ -58,6 +58,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_rng_init.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
     lib.orc_rng_init_xorwow.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int]
     lib.orc_rng_init_xorwow.restype = None
+    lib.orc_rng_init_offset.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]
+    lib.orc_rng_init_offset.restype = None
     lib.orc_rng_next.argtypes = [C.c_void_p]
     lib.orc_rng_next.restype = C.c_uint32
     lib.orc_rng_uniform.argtypes = [C.c_void_p]
@@ -79,6 +81,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.orc_accept.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.orc_accept.restype = C.c_int
+    lib.orc_accept_at.argtypes = [C.c_double, C.c_double, C.c_double, C.c_void_p]
+    lib.orc_accept_at.restype = C.c_int
     _lib = lib
     return lib
 
@@ -119,24 +123,27 @@ def costs(room, cfg=None) -> np.ndarray:
 
 class OrcOptions(C.Structure):  # mh_options, include/mh_kernel.h
     _fields_ = [("seed", C.c_uint64), ("track_best", C.c_int32), ("rng", C.c_int32),
+                ("n_temps", C.c_int32), ("swap_interval", C.c_int32), ("beta_min", C.c_double),
                 ("reserved", C.c_int32 * 4)]
 
 
 def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int = 0,
-               threads: int = 1, state: bool = False, track: int = 0, rng: int = 0):
+               threads: int = 1, state: bool = False, track: int = 0, rng: int = 0,
+               temps: int = 1, swap_interval: int = 1, beta_min: float = 2.0):
     """Runs the restated chain loop. Returns (points [chains,N,6] float32 or state
     [chains,N,6] float64 (x,y,z,rotX,rotY,rotZ), costs [chains,8] float32, accepted [chains]
     int64). `track` = 1 / 2 returns each chain's lowest / highest-total configuration instead
     of its final one (the reference's commented-out cfgBest, Kernel.cu:779-816). `rng` = 1
-    draws from cuRAND's XORWOW seeded as the reference seeds it (mh_options.rng)."""
+    draws from cuRAND's XORWOW seeded as the reference seeds it (mh_options.rng). `temps` > 1
+    runs parallel tempering (mh_options.n_temps); outputs are then in rung order per group."""
     lib = load()
     n = room.n
     cs = (C.c_float * (8 * chains))()
     acc = (C.c_int64 * chains)()
-    if track or rng:
+    if track or rng or temps > 1:
         state = True
         buf = (C.c_uint8 * (72 * n * chains))()
-        opts = OrcOptions(seed, track, rng)
+        opts = OrcOptions(seed, track, rng, temps, swap_interval, beta_min)
         rc = lib.orc_run_chains_ex(C.byref(orc_room(room)), C.cast(room.cfg, C.c_void_p),
                                    C.byref(opts), chain_begin, chains, iterations, threads,
                                    C.cast(buf, C.c_void_p), C.cast(cs, C.c_void_p), acc)

@@ -245,6 +245,15 @@ float orc_rng_normal(orc_rng* r) {
     return (float)(rad * sin(ang));
 }
 
+/* rocrand_init(seed, subsequence, offset) for Philox4x32-10. */
+void orc_rng_init_offset(orc_rng* r, uint64_t seed, uint64_t subsequence, uint64_t offset) {
+    orc_rng_init(r, seed, subsequence);
+    r->counter[0] = (uint32_t)(offset >> 2);
+    r->counter[1] = (uint32_t)(offset >> 34);
+    r->substate = (uint32_t)(offset & 3);
+    rng_refill(r);
+}
+
 void orc_philox_stream(uint64_t seed, uint64_t subsequence, uint32_t* out, int n) {
     orc_rng r;
     orc_rng_init(&r, seed, subsequence);
@@ -594,6 +603,13 @@ int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
     return u < a;
 }
 
+/* Accept at inverse temperature beta (parallel tempering; beta = BETA is Accept itself). */
+int orc_accept_at(double cost_star, double cost_cur, double beta, orc_rng* r) {
+    float u = orc_rng_uniform(r);
+    float a = fminf(1.0f, (float)exp(beta * (cost_star - cost_cur)));
+    return u < a;
+}
+
 /* ------------------------------------------------------------------------------------------
  * Validation (the reference performs none; see mh_kernel.h).
  * ---------------------------------------------------------------------------------------- */
@@ -645,91 +661,186 @@ typedef struct {
     int iterations;
     int track; /* MH_TRACK_* */
     int rng;   /* MH_RNG_* */
+    int n_temps, swap_interval;
+    const double* ladder;
     point* out_points;
     positionAndRotation* out_state;
     resultCosts* out_costs;
     int64_t* out_accepted;
 } chain_job;
 
-static void run_one(const chain_job* job, int64_t local, positionAndRotation* cur,
-                    positionAndRotation* star, positionAndRotation* best) {
-    const int n = job->room->srf->nObjs;
+/* One chain's state between steps. */
+typedef struct {
+    positionAndRotation *cur, *star, *best;
+    resultCosts cc, bc;
     orc_rng r;
+    int64_t acc;
+    int rung;
+} chain_state;
+
+static void chain_alloc(chain_state* st, int n) {
+    st->cur = malloc(sizeof(positionAndRotation) * n);
+    st->star = malloc(sizeof(positionAndRotation) * n);
+    st->best = malloc(sizeof(positionAndRotation) * n);
+}
+
+static void chain_free(chain_state* st) {
+    free(st->cur);
+    free(st->star);
+    free(st->best);
+}
+
+static void chain_init(const chain_job* job, int64_t local, chain_state* st) {
+    const int n = job->room->srf->nObjs;
     const uint64_t gid = (uint64_t)(job->chain_begin + local);
     if (job->rng == MH_RNG_CURAND_XORWOW) /* curand_init(seed + tid, tid, 0), Kernel.cu:159 */
-        orc_rng_init_xorwow(&r, (uint32_t)(job->seed + gid), gid, ORC_XORWOW_CURAND);
+        orc_rng_init_xorwow(&st->r, (uint32_t)(job->seed + gid), gid, ORC_XORWOW_CURAND);
     else
-        orc_rng_init(&r, job->seed, gid);
-    memcpy(cur, job->cfg, sizeof(positionAndRotation) * n);
-    resultCosts cc, sc;
-    orc_costs(job->room, cur, &cc);
+        orc_rng_init(&st->r, job->seed, gid);
+    memcpy(st->cur, job->cfg, sizeof(positionAndRotation) * n);
+    orc_costs(job->room, st->cur, &st->cc);
     /* Best-of-chain, the reference's commented-out intent: cfgBest := cfgCurrent
      * (Kernel.cu:779-782); star replaces best when it improves, before Accept (:808-816). */
-    resultCosts bc = cc;
-    if (job->track) memcpy(best, cur, sizeof(positionAndRotation) * n);
-    int64_t acc = 0;
-    for (int it = 0; it < job->iterations; ++it) {
-        memcpy(star, cur, sizeof(positionAndRotation) * n);
-        orc_propose(job->room, star, &r);
-        orc_costs(job->room, star, &sc);
-        if (job->track && (job->track == MH_TRACK_LOWEST ? sc.totalCosts < bc.totalCosts
-                                                         : sc.totalCosts > bc.totalCosts)) {
-            memcpy(best, star, sizeof(positionAndRotation) * n);
-            bc = sc;
+    st->bc = st->cc;
+    if (job->track) memcpy(st->best, st->cur, sizeof(positionAndRotation) * n);
+    st->acc = 0;
+    st->rung = 0;
+}
+
+/* `steps` iterations of Kernel.cu:785-828 (full copies) at inverse temperature beta. */
+static void chain_steps(const chain_job* job, chain_state* st, int steps, double beta) {
+    const int n = job->room->srf->nObjs;
+    resultCosts sc;
+    for (int it = 0; it < steps; ++it) {
+        memcpy(st->star, st->cur, sizeof(positionAndRotation) * n);
+        orc_propose(job->room, st->star, &st->r);
+        orc_costs(job->room, st->star, &sc);
+        if (job->track && (job->track == MH_TRACK_LOWEST ? sc.totalCosts < st->bc.totalCosts
+                                                         : sc.totalCosts > st->bc.totalCosts)) {
+            memcpy(st->best, st->star, sizeof(positionAndRotation) * n);
+            st->bc = sc;
         }
-        if (orc_accept(sc.totalCosts, cc.totalCosts, &r)) {
-            memcpy(cur, star, sizeof(positionAndRotation) * n);
-            cc = sc;
-            ++acc;
+        if (orc_accept_at(sc.totalCosts, st->cc.totalCosts, beta, &st->r)) {
+            positionAndRotation* t = st->cur;
+            st->cur = st->star;
+            st->star = t;
+            st->cc = sc;
+            ++st->acc;
         }
     }
-    if (job->track) { /* the output is cfgBest / bestCosts (Kernel.cu:840-860, commented out) */
-        memcpy(cur, best, sizeof(positionAndRotation) * n);
-        cc = bc;
-    }
+}
+
+static void chain_output(const chain_job* job, const chain_state* st, int64_t slot,
+                         int64_t local) {
+    const int n = job->room->srf->nObjs;
+    /* with tracking the output is cfgBest / bestCosts (Kernel.cu:840-860, commented out) */
+    const positionAndRotation* out = job->track ? st->best : st->cur;
+    const resultCosts oc = job->track ? st->bc : st->cc;
     if (job->out_points) {
-        point* p = job->out_points + local * n;
+        point* p = job->out_points + slot * n;
         for (int i = 0; i < n; ++i) {
-            p[i].x = (float)cur[i].x; p[i].y = (float)cur[i].y; p[i].z = (float)cur[i].z;
-            p[i].rotX = (float)cur[i].rotX; p[i].rotY = (float)cur[i].rotY;
-            p[i].rotZ = (float)cur[i].rotZ;
+            p[i].x = (float)out[i].x; p[i].y = (float)out[i].y; p[i].z = (float)out[i].z;
+            p[i].rotX = (float)out[i].rotX; p[i].rotY = (float)out[i].rotY;
+            p[i].rotZ = (float)out[i].rotZ;
         }
     }
-    if (job->out_state) memcpy(job->out_state + local * n, cur, sizeof(positionAndRotation) * n);
-    if (job->out_costs) job->out_costs[local] = cc;
-    if (job->out_accepted) job->out_accepted[local] = acc;
+    if (job->out_state) memcpy(job->out_state + slot * n, out, sizeof(positionAndRotation) * n);
+    if (job->out_costs) job->out_costs[slot] = oc;
+    if (job->out_accepted) job->out_accepted[local] = st->acc;
+}
+
+static void run_one(const chain_job* job, int64_t local, chain_state* st) {
+    chain_init(job, local, st);
+    chain_steps(job, st, job->iterations, ORC_BETA);
+    chain_output(job, st, local, local);
+}
+
+/* Parallel tempering (mh_options.n_temps = K > 1): group g = local chains [g*K, (g+1)*K).
+ * Replicas step independently at their rung's beta; after every swap_interval steps, exchange
+ * round t tries the rung pairs (k, k+1), k = (t-1) mod 2 + 2i, with the Philox uniform of
+ * (seed, subsequence 2^63 + global group, offset (t-1)*K + k) against
+ * min(1, (float)exp((beta_k - beta_k+1) * (E_k+1 - E_k))). Output slot g*K + final rung. */
+static void run_group(const chain_job* job, int64_t g, chain_state* st) {
+    const int K = job->n_temps;
+    int perm[1024];
+    for (int j = 0; j < K; ++j) {
+        chain_init(job, g * K + j, &st[j]);
+        st[j].rung = j;
+        perm[j] = j;
+    }
+    const uint64_t gid = (uint64_t)(job->chain_begin / K + g);
+    int64_t done = 0;
+    while (done < job->iterations) {
+        int chunk = job->iterations - (int)done;
+        const int to_round = job->swap_interval - (int)(done % job->swap_interval);
+        if (to_round < chunk) chunk = to_round;
+        for (int j = 0; j < K; ++j) chain_steps(job, &st[j], chunk, job->ladder[st[j].rung]);
+        done += chunk;
+        if (done % job->swap_interval == 0) {
+            const int64_t round = done / job->swap_interval;
+            for (int k = (int)((round - 1) & 1); k + 1 < K; k += 2) {
+                const int ca = perm[k], cb = perm[k + 1];
+                orc_rng u_r;
+                orc_rng_init_offset(&u_r, job->seed, (1ull << 63) | gid,
+                                    (uint64_t)(round - 1) * K + k);
+                const float u = orc_rng_uniform(&u_r);
+                const double db = job->ladder[k] - job->ladder[k + 1];
+                const float thr = fminf(1.0f, (float)exp(db * ((double)st[cb].cc.totalCosts -
+                                                               (double)st[ca].cc.totalCosts)));
+                if (u < thr) {
+                    perm[k] = cb;
+                    perm[k + 1] = ca;
+                    st[ca].rung = k + 1;
+                    st[cb].rung = k;
+                }
+            }
+        }
+    }
+    for (int j = 0; j < K; ++j) chain_output(job, &st[j], g * K + st[j].rung, g * K + j);
 }
 
 static void* chain_worker(void* arg) {
     const chain_job* job = (const chain_job*)arg;
     const int n = job->room->srf->nObjs;
-    positionAndRotation* cur = malloc(sizeof(positionAndRotation) * n);
-    positionAndRotation* star = malloc(sizeof(positionAndRotation) * n);
-    positionAndRotation* best = malloc(sizeof(positionAndRotation) * n);
-    for (int64_t c = job->lo; c < job->hi; ++c) run_one(job, c, cur, star, best);
-    free(cur);
-    free(star);
-    free(best);
+    const int K = job->n_temps > 1 ? job->n_temps : 1;
+    chain_state* st = calloc((size_t)K, sizeof(chain_state));
+    for (int j = 0; j < K; ++j) chain_alloc(&st[j], n);
+    if (K > 1)  /* lo/hi count groups */
+        for (int64_t g = job->lo; g < job->hi; ++g) run_group(job, g, st);
+    else
+        for (int64_t c = job->lo; c < job->hi; ++c) run_one(job, c, &st[0]);
+    for (int j = 0; j < K; ++j) chain_free(&st[j]);
+    free(st);
     return NULL;
 }
 
-static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
-                      int track, int rng, int64_t chain_begin, int64_t n_chains, int iterations,
-                      int nthreads,
+static int run_chains(const orc_room* room, const positionAndRotation* cfg, const mh_options* o,
+                      int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                       point* out_points, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted) {
     if (orc_validate(room, cfg) != 0) return -1;
     if (n_chains < 0 || iterations < 0) return fail("negative chain or step count%ld", 0);
-    if (track < MH_TRACK_OFF || track > MH_TRACK_HIGHEST) return fail("bad track_best %ld", track);
-    if (rng < MH_RNG_PHILOX || rng > MH_RNG_CURAND_XORWOW) return fail("bad rng %ld", rng);
+    if (o->track_best < MH_TRACK_OFF || o->track_best > MH_TRACK_HIGHEST)
+        return fail("bad track_best %ld", o->track_best);
+    if (o->rng < MH_RNG_PHILOX || o->rng > MH_RNG_CURAND_XORWOW) return fail("bad rng %ld", o->rng);
+    const int K = o->n_temps > 1 ? o->n_temps : 1;
+    if (K > 1024) return fail("n_temps %ld > 1024", K);
+    if (K > 1 && (n_chains % K || chain_begin % K || o->swap_interval < 1 ||
+                  !(o->beta_min > 0.0) || !(o->beta_min <= ORC_BETA)))
+        return fail("bad parallel tempering options (n_temps %ld)", K);
+    double ladder[1024];
+    for (int k = 0; k < K; ++k) /* geometric from BETA (rung 0) down to beta_min */
+        ladder[k] = k == 0 ? ORC_BETA : ORC_BETA * pow(o->beta_min / ORC_BETA, (double)k / (K - 1));
+    const int64_t units = n_chains / K; /* chains, or tempering groups */
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > n_chains) nthreads = (int)(n_chains > 0 ? n_chains : 1);
+    if (nthreads > units) nthreads = (int)(units > 0 ? units : 1);
     chain_job* jobs = calloc((size_t)nthreads, sizeof(chain_job));
     pthread_t* th = calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; ++t) {
-        chain_job j = {room, cfg, seed, chain_begin,
-                       n_chains * t / nthreads, n_chains * (t + 1) / nthreads,
-                       iterations, track, rng, out_points, out_state, out_costs, out_accepted};
+        chain_job j = {room, cfg, o->seed, chain_begin,
+                       units * t / nthreads, units * (t + 1) / nthreads,
+                       iterations, o->track_best, o->rng, K, o->swap_interval, ladder,
+                       out_points, out_state, out_costs, out_accepted};
         jobs[t] = j;
     }
     for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, chain_worker, &jobs[t]);
@@ -740,25 +851,37 @@ static int run_chains(const orc_room* room, const positionAndRotation* cfg, uint
     return 0;
 }
 
+static mh_options plain_options(uint64_t seed) {
+    mh_options o;
+    memset(&o, 0, sizeof o);
+    o.seed = seed;
+    o.n_temps = 1;
+    o.swap_interval = 1;
+    o.beta_min = ORC_BETA;
+    return o;
+}
+
 int orc_run_chains(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                    int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                    point* out_points, resultCosts* out_costs, int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, MH_TRACK_OFF, MH_RNG_PHILOX, chain_begin, n_chains,
-                      iterations, nthreads, out_points, NULL, out_costs, out_accepted);
+    const mh_options o = plain_options(seed);
+    return run_chains(room, cfg, &o, chain_begin, n_chains, iterations, nthreads, out_points,
+                      NULL, out_costs, out_accepted);
 }
 
 int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, uint64_t seed,
                          int64_t chain_begin, int64_t n_chains, int iterations, int nthreads,
                          positionAndRotation* out_state, resultCosts* out_costs,
                          int64_t* out_accepted) {
-    return run_chains(room, cfg, seed, MH_TRACK_OFF, MH_RNG_PHILOX, chain_begin, n_chains,
-                      iterations, nthreads, NULL, out_state, out_costs, out_accepted);
+    const mh_options o = plain_options(seed);
+    return run_chains(room, cfg, &o, chain_begin, n_chains, iterations, nthreads, NULL,
+                      out_state, out_costs, out_accepted);
 }
 
 int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       const mh_options* opts, int64_t chain_begin, int64_t n_chains,
                       int iterations, int nthreads, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted) {
-    return run_chains(room, cfg, opts->seed, opts->track_best, opts->rng, chain_begin, n_chains,
-                      iterations, nthreads, NULL, out_state, out_costs, out_accepted);
+    return run_chains(room, cfg, opts, chain_begin, n_chains, iterations, nthreads, NULL,
+                      out_state, out_costs, out_accepted);
 }

@@ -79,6 +79,8 @@ void orc_philox_stream(uint64_t seed, uint64_t subsequence, uint32_t* out, int n
  * rocRAND engine's equivalent (ORC_XORWOW_ROCRAND). orc_rng_next / _uniform / _normal then draw
  * curand(), curand_uniform() and curand_normal(). */
 void orc_rng_init_xorwow(orc_rng* r, uint64_t seed, uint64_t subsequence, int kind);
+/* Philox stream (seed, subsequence) started at draw `offset` (rocrand_init's offset). */
+void orc_rng_init_offset(orc_rng* r, uint64_t seed, uint64_t subsequence, uint64_t offset);
 /* Random123 philox4x32 with 10 rounds on one (counter, key) block, for KAT vectors. */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
@@ -91,6 +93,8 @@ int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r);
 void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r);
 /* Accept rule of Kernel.cu:706-713. */
 int orc_accept(double cost_star, double cost_cur, orc_rng* r);
+/* The same at inverse temperature beta (parallel tempering). */
+int orc_accept_at(double cost_star, double cost_cur, double beta, orc_rng* r);
 
 /* Runs chains [chain_begin, chain_begin + n_chains) of the defined single-proposer chain
  * (Kernel.cu:777-828) for `iterations` steps on `nthreads` host threads. out_points holds
@@ -111,7 +115,9 @@ int orc_run_chains_state(const orc_room* room, const positionAndRotation* cfg, u
  * best-of-chain tracking. With tracking on, out_state / out_costs hold each chain's best
  * configuration and its costs. */
 /* opts->rng == MH_RNG_CURAND_XORWOW: chain c draws from curand_init((uint32_t)(seed + c), c, 0)
- * as Kernel.cu:151-159,943 seeds thread c. */
+ * as Kernel.cu:151-159,943 seeds thread c. opts->n_temps > 1: parallel tempering as
+ * KernelWrapperEx defines it (include/mh_kernel.h); outputs are in rung order per group
+ * (out_accepted stays in chain order). */
 int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       const mh_options* opts, int64_t chain_begin, int64_t n_chains,
                       int iterations, int nthreads, positionAndRotation* out_state,

@@ -372,7 +372,7 @@ def test_best_of_chain_kernel_wrapper_ex(mh, orc, hiplib):
     p0, c0 = mh.kernel_wrapper(room, chains, steps, seed=seed)
     lib = mh.load_library()
     g = mh.abi.gpuConfig(chains, 0, 64, 0, 0, steps)
-    res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh.abi.mh_options(seed, 0)))
+    res = lib.KernelWrapperEx(*room.args(), C.byref(g), C.byref(mh.abi.options(seed)))
     assert res
     try:
         pts = (mh.abi.point * (chains * room.n)).from_address(C.cast(res[0].points, C.c_void_p).value)
@@ -508,3 +508,69 @@ def test_oversized_room_is_rejected(mh, hiplib):
     room = mh.synthetic_room(513)
     with pytest.raises(mh.MHError, match="too large"):
         mh.kernel_wrapper(room, 4, 10, seed=1)
+
+
+# ---- parallel tempering (mh_options.n_temps > 1) ---------------------------------------------
+
+@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("kind,n,K,chains,steps,interval", [
+    ("main", 32, 4, 64, 300, 25),
+    ("syn", 9, 2, 128, 400, 1),       # an exchange round after every step
+    ("syn", 16, 8, 64, 1200, 250),    # rounds and 1000-step launches interleave
+    ("frozen", 16, 3, 48, 300, 7),
+    ("syn", 64, 4, 32, 400, 100),
+])
+def test_tempering_matches_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, K, chains, steps,
+                                  interval):
+    """Replica exchange on the device (per-chain beta in both step kernels, mh_exchange_kernel
+    between launches) against the oracle's restatement, bit for bit, outputs in rung order."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    room = _room(mh, kind, n)
+    seed = 3100 + n + K
+    with mh.Session(room, chains, seed=seed, temps=K, swap_interval=interval, beta_min=0.2) as s:
+        assert s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_state, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8, temps=K,
+                                             swap_interval=interval, beta_min=0.2)
+    same = np.all(pts.view(np.uint32) == ref_state.astype(np.float32).view(np.uint32),
+                  axis=(1, 2)) & np.all(costs.view(np.uint32) == ref_costs.view(np.uint32), axis=1)
+    print(f"tempering {step} {kind} N={n} K={K}: {same.mean() * 100:.2f}% bit-identical")
+    assert same.mean() >= 0.99
+
+
+def test_tempering_resume_and_wrapper(mh, orc, hiplib):
+    """Two session runs (600 + 600 steps) equal one of 1200 (the exchange schedule counts steps
+    across calls), KernelWrapperEx with the same options equals the session, and tempering with
+    best-of-chain tracking and the XORWOW stream together matches the oracle."""
+    room = mh.synthetic_room(24)
+    K, chains, seed, iv = 4, 64, 51, 150
+    with mh.Session(room, chains, seed=seed, temps=K, swap_interval=iv, beta_min=0.5) as s:
+        s.run(1200)
+        s.finalize()
+        p1, c1 = s.download()
+    with mh.Session(room, chains, seed=seed, temps=K, swap_interval=iv, beta_min=0.5) as s:
+        s.run(600)
+        s.run(600)
+        s.finalize()
+        p2, c2 = s.download()
+    assert np.array_equal(p1.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))
+    p3, c3 = mh.kernel_wrapper(room, chains, 1200, seed=seed, temps=K, swap_interval=iv,
+                               beta_min=0.5)
+    assert np.array_equal(p1.view(np.uint32), p3.view(np.uint32))
+    p4, c4 = mh.kernel_wrapper(room, chains, 500, seed=seed, temps=K, swap_interval=iv,
+                               beta_min=0.5, track=2, rng=1)
+    st, rc, _ = orc.run_chains(room, chains, 500, seed, threads=8, temps=K, swap_interval=iv,
+                               beta_min=0.5, track=2, rng=1)
+    assert np.array_equal(p4.view(np.uint32), st.astype(np.float32).view(np.uint32))
+    assert np.array_equal(c4.view(np.uint32), rc.view(np.uint32))
+
+
+def test_tempering_validation(mh, hiplib):
+    room = mh.synthetic_room(8)
+    with pytest.raises(mh.MHError, match="multiple of n_temps"):
+        mh.kernel_wrapper(room, 10, 10, seed=1, temps=4, swap_interval=5, beta_min=0.5)
+    with pytest.raises(mh.MHError, match="beta_min"):
+        mh.kernel_wrapper(room, 8, 10, seed=1, temps=4, swap_interval=5, beta_min=3.0)

@@ -343,3 +343,73 @@ def test_xorwow_curand_formulas(orc):
     assert list(z.xw) == [(6615241 + t1 + t0) & 0xffffffff, (123456789 + t0) & 0xffffffff,
                           362436069 ^ t0, (521288629 + t1) & 0xffffffff, 88675123 ^ t1,
                           (5783321 + t0) & 0xffffffff]
+
+
+def _ladder(K, beta_min):
+    return [2.0 if k == 0 else 2.0 * math.pow(beta_min / 2.0, k / (K - 1)) for k in range(K)]
+
+
+@pytest.mark.parametrize("K,interval,steps", [(3, 5, 31), (4, 1, 12), (2, 40, 40)])
+def test_tempering_restatement(mh, orc, K, interval, steps):
+    """orc_run_chains_ex's parallel tempering against the rule written out here step by step
+    (include/mh_kernel.h KernelWrapperEx): replicas step at their rung's beta; after every
+    `interval` steps round t tries the pairs (k, k+1), k = (t-1) mod 2 + 2i, with the Philox
+    uniform of (seed, 2^63 + group, (t-1)*K + k); outputs land in rung order."""
+    lib = orc.load()
+    room = mh.synthetic_room(8)
+    seed, groups, beta_min = 77, 2, 0.25
+    chains = groups * K
+    st, costs, acc = orc.run_chains(room, chains, steps, seed, temps=K, swap_interval=interval,
+                                    beta_min=beta_min)
+    lad = _ladder(K, beta_min)
+    orm = orc.orc_room(room)
+    for g in range(groups):
+        reps = []
+        for j in range(K):
+            r = orc.rng_init(seed, g * K + j)
+            cur = mh.clone_cfg(room)
+            reps.append({"r": r, "cur": cur, "cc": orc.costs(room, cur), "rung": j})
+        perm = list(range(K))
+        done = 0
+        while done < steps:
+            chunk = min(steps - done, interval - done % interval)
+            for rep_ in reps:
+                for _ in range(chunk):
+                    star = _copy(rep_["cur"])
+                    lib.orc_propose(C.byref(orm), C.cast(star, C.c_void_p), C.byref(rep_["r"]))
+                    sc = orc.costs(room, star)
+                    if lib.orc_accept_at(float(sc[0]), float(rep_["cc"][0]), lad[rep_["rung"]],
+                                         C.byref(rep_["r"])):
+                        rep_["cur"], rep_["cc"] = star, sc
+            done += chunk
+            if done % interval == 0:
+                t = done // interval
+                for k in range((t - 1) % 2, K - 1, 2):
+                    a, b = perm[k], perm[k + 1]
+                    ur = orc.OrcRng()
+                    lib.orc_rng_init_offset(C.byref(ur), seed, (1 << 63) | g, (t - 1) * K + k)
+                    u = lib.orc_rng_uniform(C.byref(ur))
+                    thr = min(np.float32(1.0), np.float32(math.exp(
+                        (lad[k] - lad[k + 1]) * (float(reps[b]["cc"][0]) - float(reps[a]["cc"][0])))))
+                    if np.float32(u) < thr:
+                        perm[k], perm[k + 1] = b, a
+                        reps[a]["rung"], reps[b]["rung"] = k + 1, k
+        for j, rep_ in enumerate(reps):
+            slot = g * K + rep_["rung"]
+            got = np.array([[b.x, b.y, b.z, b.rotX, b.rotY, b.rotZ] for b in rep_["cur"]])
+            assert np.array_equal(got, st[slot])
+            assert np.array_equal(rep_["cc"].view(np.uint32), costs[slot].view(np.uint32))
+
+
+def test_tempering_at_one_temperature_permutes_plain_chains(mh, orc):
+    """With beta_min = BETA every rung runs the reference's chain, so every exchange is accepted
+    (threshold 1) and the outputs are the plain chains, permuted within each group."""
+    room = mh.synthetic_room(16)
+    K, chains, steps, seed = 4, 16, 60, 9
+    st, costs, _ = orc.run_chains(room, chains, steps, seed, temps=K, swap_interval=7,
+                                  beta_min=2.0)
+    pst, pcosts, _ = orc.run_chains(room, chains, steps, seed, state=True)
+    for g in range(chains // K):
+        a = sorted(costs[g * K:(g + 1) * K].view(np.uint32).tolist())
+        b = sorted(pcosts[g * K:(g + 1) * K].view(np.uint32).tolist())
+        assert a == b
