@@ -127,9 +127,17 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    # One process per GPU over RCCL. $MH_BENCH_BACKEND=gloo rehearses the multi-rank path on a
+    # box with fewer GPUs than ranks (ranks then share devices round-robin; CPU-side collectives).
+    backend = os.environ.get("MH_BENCH_BACKEND", "nccl")
+    device = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    cdev = f"cuda:{device}" if backend == "nccl" else "cpu"
 
     mh = graft.load_package()
     mh.load_library()
@@ -142,7 +150,7 @@ def main() -> int:
     handle = stream.cuda_stream
     assert handle, "need a non-null HIP stream handle"
     offset, count = shard(rank, args.chains)
-    sess = mh.Session(room, count, seed=args.seed, device=local_rank, chain_offset=offset)
+    sess = mh.Session(room, count, seed=args.seed, device=device, chain_offset=offset)
     lanes, cpw, step_kernel = sess.step_kernel()
 
     for _ in range(args.warmup):
@@ -171,8 +179,8 @@ def main() -> int:
     s = sess.summary()
     rec = torch.tensor(summary_record(s.sum_total, s.best_total, s.best_chain, s.n_chains,
                                       s.accepted), dtype=torch.float64,
-                       device=f"cuda:{local_rank}")
-    times = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
+                       device=cdev)
+    times = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=cdev)
     if world > 1:
         gathered = [torch.empty_like(rec) for _ in range(world)]
         dist.all_gather(gathered, rec)
