@@ -83,6 +83,7 @@ struct ChainPtrs {
     float4* OFF;
     float4* CLA;
     ChainAux* aux;
+    const DevRoom* rm;  // LDS copy of the room scalars
 };
 
 // ---- compacted term lists for the ordered sums -------------------------------------------
@@ -160,8 +161,10 @@ template <int L, int NPL, bool WITH_OL, bool DELTA>
 __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb) {
-    const DevRoom& rm = a.rm;
-    const int n = rm.n, c = rm.c;
+    // The room scalars are read from the workgroup's LDS copy where they are used, not kept
+    // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
+    const DevRoom& rm = *ch.rm;
+    const int n = a.rm.n, c = a.rm.c;
 
     unsigned long long t0 = 0;
     MH_STAMP(t0);
@@ -864,6 +867,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     }
     for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) relc_l[i] = a.relc[i];
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
+    DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + a.lay.h_room);
+    if (threadIdx.x == 0) *rm_l = a.rm;
     __syncthreads();
 
     const int64_t chain = ((int64_t)blockIdx.x * waves_per_wg + wave) * G + g;
@@ -890,6 +895,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
     ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
+    ch.rm = rm_l;
 
     // Zero the dense replay streams past N (never written afterwards).
     for (int i = n + r; i < a.lay.N4; i += L) {
@@ -960,7 +966,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         for (int it = 0; it < a.iterations; ++it) {
             unsigned long long ts = 0;
             MH_STAMP(ts);
-            const int2 kk = propose(rng, a.rm, frozen, ch, writer);
+            const int2 kk = propose(rng, *rm_l, frozen, ch, writer);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
