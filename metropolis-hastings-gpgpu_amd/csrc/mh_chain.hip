@@ -851,10 +851,11 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     const int waves_per_wg = blockDim.x >> 6;
 
     // Room tables: staged once per workgroup (the chain loop then never touches global memory).
-    RectShape* objs_l = reinterpret_cast<RectShape*>(lds + a.lay.h_obj);
-    RectShape* clrs_l = reinterpret_cast<RectShape*>(lds + a.lay.h_clr);
+    constexpr FixedLds F = fixed_lds(L, NPL);  // compile-time part of the layout
+    RectShape* objs_l = reinterpret_cast<RectShape*>(lds + F.h_obj);
+    RectShape* clrs_l = reinterpret_cast<RectShape*>(lds + F.h_clr);
     RelConst* relc_l = reinterpret_cast<RelConst*>(lds + a.lay.h_rel);
-    unsigned char* frozen = lds + a.lay.h_frz;
+    unsigned char* frozen = lds + F.h_frz;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         RectShape s = a.objc[i].off;
         s.pad = __float_as_int(a.objc[i].area);
@@ -867,7 +868,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     }
     for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) relc_l[i] = a.relc[i];
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
-    DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + a.lay.h_room);
+    DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + F.h_room);
     if (threadIdx.x == 0) *rm_l = a.rm;
     __syncthreads();
 
@@ -879,22 +880,22 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.objs = objs_l;
     ch.clrs = clrs_l;
     ch.relc = relc_l;
-    ch.P = reinterpret_cast<ObjP*>(base + a.lay.P);
-    ch.RY = reinterpret_cast<double*>(base + a.lay.RY);
-    ch.PX = reinterpret_cast<double*>(base + a.lay.PX);
-    ch.PY = reinterpret_cast<double*>(base + a.lay.PY);
-    ch.CPHF = reinterpret_cast<float*>(base + a.lay.CPHF);
-    ch.RMXF = reinterpret_cast<float*>(base + a.lay.RMXF);
-    ch.LCL = reinterpret_cast<float*>(base + a.lay.LCL);
+    ch.P = reinterpret_cast<ObjP*>(base + F.P);
+    ch.RY = reinterpret_cast<double*>(base + F.RY);
+    ch.PX = reinterpret_cast<double*>(base + F.PX);
+    ch.PY = reinterpret_cast<double*>(base + F.PY);
+    ch.CPHF = reinterpret_cast<float*>(base + F.CPHF);
+    ch.RMXF = reinterpret_cast<float*>(base + F.RMXF);
+    ch.LCL = reinterpret_cast<float*>(base + F.LCL);
     ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
     ch.lst_r = a.lay.lst_r;
     ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
-    ch.X = reinterpret_cast<double*>(base + a.lay.X);
-    ch.Y = reinterpret_cast<double*>(base + a.lay.Y);
+    ch.X = reinterpret_cast<double*>(base + F.X);
+    ch.Y = reinterpret_cast<double*>(base + F.Y);
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
     ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
-    ch.aux = reinterpret_cast<ChainAux*>(base + a.lay.AUX);
+    ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
 
     // Zero the dense replay streams past N (never written afterwards).

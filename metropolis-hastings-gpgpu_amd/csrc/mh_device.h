@@ -252,40 +252,91 @@ inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h
     return h;
 }
 
-// with_off: the layout of the passes that evaluate OffLimitsCosts (final state, evaluation).
-inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off = false) {
-    ChainLds l;
-    int h = 0;
-    l.h_obj = h;  h += round16((int)sizeof(RectShape) * n);
-    l.h_clr = h;  h += round16((int)sizeof(RectShape) * (c > 0 ? c : 1));
-    l.h_rel = h;  h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
-    l.h_frz = h;  h += round16(n + 1);
-    l.h_room = h; h += round16((int)sizeof(DevRoom));
-    l.hdr = h;
+// Objects per lane of the full-evaluation kernel instance that serves npl (mh_chain.hip launch()).
+inline MH_HD constexpr int npl_instance(int npl) { return npl <= 1 ? 1 : npl <= 2 ? 2 : npl <= 4 ? 4 : 8; }
+
+inline MH_HD constexpr int round16c(int v) { return (v + 15) & ~15; }
+
+inline MH_HD constexpr int bank_place_c(int o, unsigned& used) {
+    o = round16c(o);
+    for (int k = 0; k < 16 && ((used >> ((o >> 4) & 15)) & 1u); ++k) o += 16;
+    used |= 1u << ((o >> 4) & 15);
+    return o;
+}
+
+// The part of the full-evaluation kernel's LDS layout that depends only on the kernel instance
+// (L lanes, NPL objects per lane: capacity NC = L * NPL objects). The kernel addresses these
+// arrays at compile-time offsets (immediate ds_read/ds_write offsets, no SGPRs); the host sizes
+// the workgroup with the same function. Header: DevRoom, object shapes, frozen flags, then the
+// clearance shapes; the relationship table follows at a run-time offset.
+struct FixedLds {
+    int h_room, h_obj, h_frz, h_clr;                    // workgroup header
+    int P, RY, X, Y, AUX, PX, PY, CPHF, RMXF, LCL, end;  // per chain
+};
+
+inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
+    const int NC = L * NPL;
+    FixedLds f{};
+    f.h_room = 0;
+    f.h_obj = round16c((int)sizeof(DevRoom));
+    f.h_frz = f.h_obj + round16c((int)sizeof(RectShape) * NC);
+    f.h_clr = f.h_frz + round16c(NC + 1);
     int o = 0;
-    l.P = o;   o += round16(16 * n);
-    l.RY = o;  o += round16(8 * n);
-    l.X = o;   o += round16(8 * n);
-    l.Y = o;   o += round16(8 * n);
+    f.P = o;   o += 16 * NC;
+    f.RY = o;  o += 8 * NC;
+    f.X = o;   o += 8 * NC;
+    f.Y = o;   o += 8 * NC;
+    f.AUX = o; o += kChainAuxBytes;
+    // The replay's streams: lanes 0, 1, 6, 7 read PX, PY, LPW, LANG with one instruction,
+    // lanes 2, 3, 4 read CPHF, RMXF, LCL with another -- each set on distinct banks.
+    unsigned dslots = 0u, fslots = 0u;
+    f.PX = bank_place_c(o, dslots);   o = f.PX + 8 * NC;
+    f.PY = bank_place_c(o, dslots);   o = f.PY + 8 * NC;
+    f.CPHF = bank_place_c(o, fslots); o = f.CPHF + 4 * NC;
+    f.RMXF = bank_place_c(o, fslots); o = f.RMXF + 4 * NC;
+    f.LCL = bank_place_c(o, fslots);  o = f.LCL + 8 * L;
+    f.end = o;
+    return f;
+}
+
+// with_off: the layout of the passes that evaluate OffLimitsCosts (final / evaluation). The
+// instance-fixed part comes from fixed_lds(); the PairWise / Angle lists, clearance boxes and
+// off-limits boxes (sized by R, C, N) follow at run-time offsets.
+inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off = false) {
+    const int NPL = npl_instance((n + L - 1) / L);
+    const FixedLds f = fixed_lds(L, NPL);
+    ChainLds l;
+    l.h_room = f.h_room;
+    l.h_obj = f.h_obj;
+    l.h_frz = f.h_frz;
+    l.h_clr = f.h_clr;
+    int h = f.h_clr + round16((int)sizeof(RectShape) * (c > 0 ? c : 1));
+    l.h_rel = h;  h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
+    l.hdr = h;
+    l.P = f.P;
+    l.RY = f.RY;
+    l.X = f.X;
+    l.Y = f.Y;
+    l.AUX = f.AUX;
+    l.PX = f.PX;
+    l.PY = f.PY;
+    l.CPHF = f.CPHF;
+    l.RMXF = f.RMXF;
+    l.LCL = f.LCL;
+    l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
+    l.N4 = (n + 3) & ~3;
+    int o = f.end;
+    unsigned dslots = 0u;  // LPW / LANG on banks apart from PX / PY
+    dslots |= 1u << ((f.PX >> 4) & 15);
+    dslots |= 1u << ((f.PY >> 4) & 15);
+    l.LPW = bank_place(o, &dslots);  o = l.LPW + 8 * l.lst_r;
+    l.LANG = bank_place(o, &dslots); o = l.LANG + 8 * l.lst_r;
+    l.CLA = round16(o);              o = l.CLA + 16 * (c > 0 ? c : 1);
     l.OFF = -1;
     if (with_off) {
         l.OFF = o;
         o += round16(16 * n);
     }
-    l.CLA = o; o += round16(16 * (c > 0 ? c : 1));
-    l.AUX = o; o += kChainAuxBytes;
-    l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
-    l.N4 = (n + 3) & ~3;
-    // The replay's streams: lanes 0, 1, 6, 7 read PX, PY, LPW, LANG with one instruction,
-    // lanes 2, 3, 4 read CPHF, RMXF, LCL with another -- each set on distinct banks.
-    unsigned dslots = 0u, fslots = 0u;
-    l.PX = bank_place(o, &dslots);   o = l.PX + 8 * l.N4;
-    l.PY = bank_place(o, &dslots);   o = l.PY + 8 * l.N4;
-    l.CPHF = bank_place(o, &fslots); o = l.CPHF + 4 * l.N4;
-    l.RMXF = bank_place(o, &fslots); o = l.RMXF + 4 * l.N4;
-    l.LCL = bank_place(o, &fslots);  o = l.LCL + 8 * L;
-    l.LPW = bank_place(o, &dslots);  o = l.LPW + 8 * l.lst_r;
-    l.LANG = bank_place(o, &dslots); o = l.LANG + 8 * l.lst_r;
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
     l.stride = o;
