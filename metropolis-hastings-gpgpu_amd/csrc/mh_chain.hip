@@ -82,6 +82,8 @@ struct ChainPtrs {
     double* zrr;      // HBM: this chain's z, rotX, rotZ rows (F_Z, F_RX, F_RZ of the pose block)
     float4* OFF;
     float4* CLA;
+    uint64_t* NZ;     // [2][C] row words of the non-zero Clearance pairs
+    int* PRE;         // [C] row prefix counts
     ChainAux* aux;
     const DevRoom* rm;  // LDS copy of the room scalars
 };
@@ -160,7 +162,7 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
 template <int L, int NPL, bool WITH_OL, bool DELTA>
 __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
-                           int kb) {
+                           int kb, ClPairs& clo, const ClPairs& clp) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
     const DevRoom& rm = *ch.rm;
@@ -510,7 +512,79 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     if (r == 0) MH_PHASE(ch, 4, t0);
     // ClearanceCosts pairs, clearance-major then object (Kernel.cu:408-431).
     int cnt_cl = 0;
+    // One object per lane: the non-zero pairs are tracked incrementally. A proposal changes
+    // the pairs of the moved objects' columns and of the rows of clearances they carry; the
+    // others keep their zero / non-zero state, so only the non-zero pairs are re-evaluated,
+    // each by its object's lane, and written straight to their list positions (row prefix +
+    // the row's set bits below the object).
+    constexpr bool INC_CL = DELTA && NPL == 1;
+    bool cl_done = false;
+    if constexpr (NPL == 1) {
+        const int j = r;
+        const float4 boxj = j < n ? shape_box(ch.objs[j], ch.P[j].xf, ch.P[j].yf)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (INC_CL) {
+            const uint64_t* NZc = ch.NZ + clp.buf * c;
+            uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
+            uint64_t cm = clp.cm;
+            uint64_t w = (r < c) ? NZc[r] : 0ull;  // lane r's clearance row, patched below
+            const int kk2[2] = {ka, kb};
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {  // the moved objects' columns, one clearance per lane
+                const int k = kk2[q];
+                if (k < 0) continue;
+                const ObjP pk = ch.P[k];
+                const float4 bk = shape_box(ch.objs[k], pk.xf, pk.yf);
+                const bool nzk = r < c && overlap(ch.CLA[r], bk) != 0.0f;
+                const uint64_t colk = group_ballot<L>(nzk, gbase);
+                if (j == k) cm = colk;
+                w = (w & ~(1ull << k)) | ((uint64_t)nzk << k);
+            }
+            // rows of the clearances whose source moved: every object lane re-tests its pair
+            uint64_t moved = group_ballot<L>(r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb),
+                                             gbase);
+            while (moved) {
+                const int i = __builtin_ctzll(moved);
+                moved &= moved - 1;
+                const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
+                const uint64_t row = group_ballot<L>(nzi, gbase);
+                cm = (cm & ~(1ull << i)) | ((uint64_t)nzi << i);
+                if (r == i) w = row;
+            }
+            if (r < c) NZn[r] = w;
+            int total;
+            const int pre = group_excl_scan<L>(r < c ? __builtin_popcountll(w) : 0, r, total);
+            if (r < c) ch.PRE[r] = pre;
+            clo.cm = cm;
+            clo.buf = clp.buf ^ 1;
+            wave_sync();
+            if (total <= 2 * L) {  // fits the list: write every term at its position
+                const uint64_t below = (1ull << j) - 1ull;
+                uint64_t bits = j < n ? cm : 0ull;
+                while (bits) {
+                    const int i = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int pos = ch.PRE[i] + __builtin_popcountll(NZn[i] & below);
+                    ch.LCL[pos] = -overlap(ch.CLA[i], boxj);
+                }
+                cnt_cl = total;
+                cl_done = true;
+            }
+        } else {
+            // full evaluation: the pair state from scratch, for the steps that follow
+            uint64_t cm = 0ull;
+            for (int i = 0; i < c; ++i) {
+                const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
+                const uint64_t row = group_ballot<L>(nzi, gbase);
+                cm |= (uint64_t)nzi << i;
+                if (r == 0) ch.NZ[i] = row;
+            }
+            clo.cm = cm;
+            clo.buf = 0;
+        }
+    }
     for (int rep = 0; rep < MH_REPS(8); ++rep) {
+    if (cl_done) break;
     MH_CLOBBER();
     cnt_cl = 0;
     float4 offb[NPL];
@@ -895,6 +969,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
     ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
+    ch.NZ = reinterpret_cast<uint64_t*>(base + a.lay.NZ);
+    ch.PRE = reinterpret_cast<int*>(base + a.lay.PRE);
     ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
 
@@ -933,7 +1009,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     float cur[8];
     SymRows<NPL> sym;  // symmetry row maxima of the current configuration
     if constexpr (OP == OP_INIT) {
-        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
+        ClPairs cl0;
+        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, cl0, cl0);
         if (r == 0) {
             ChainMeta m;
             m.draws = 0;
@@ -958,7 +1035,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
         double beta = kBeta;
         if constexpr (TRACK)  // (the extended families also carry parallel tempering)
             if (a.n_temps > 1) beta = a.ladder[m0.rung];
-        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
+        ClPairs cl;  // non-zero Clearance pairs of the current configuration
+        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, cl, cl);
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 8; ++k) ch.aux->cyc[k] = 0;
@@ -972,7 +1050,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
             SymRows<NPL> ss;
-            eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y);
+            ClPairs cls;
+            eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y, cls, cl);
             MH_STAMP(ts);
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if constexpr (TRACK) {
@@ -987,6 +1066,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             if (acc) {
                 cur_total = sc[0];
                 sym = ss;
+                cl = cls;
                 ++accepted;
                 if (writer) {
                     for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
@@ -1015,7 +1095,8 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
             a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
-        eval_costs<L, NPL, true, false>(a, ch, r, gbase, cur, sym, sym, -1, -1);
+        ClPairs clf;
+        eval_costs<L, NPL, true, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, clf, clf);
         if (r == 0) {
             resultCosts rc;
             rc.totalCosts = cur[0];

@@ -491,6 +491,14 @@ struct SymRows {
     int arg[NPL];
 };
 
+// Non-zero Clearance pairs of a configuration, for the incremental pair update of the
+// full-evaluation step (one object per lane): this lane's column mask (bit i: clearance i
+// overlaps the lane's object) and which of the two LDS row-word buffers holds the rows.
+struct ClPairs {
+    uint64_t cm;
+    int buf;
+};
+
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
 __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, double& tpw,
                                           double& tang) {

@@ -148,6 +148,9 @@ struct ChainLds {
     int X, Y;    // double[N]   (z, rotX, rotZ never enter a cost: they stay in HBM)
     int OFF;     // float4[N] off-limits boxes (final / evaluation passes only; -1 in the step)
     int CLA;     // float4[C] clearance boxes at their source objects
+    int NZ;      // uint64[2][C] non-zero Clearance pairs per clearance row (bit j: object j),
+                 // current / proposed (incremental pairs, one object per lane)
+    int PRE;     // int[C] row prefix counts of the proposed rows
     int AUX;     // ChainAux: proposal backups and the current costs
     int PX, PY;    // double[N4] per-object VisualBalance products (N4 = round4(N), zero past N)
     int CPHF, RMXF;  // float[N4] per-object -cos(phi) and -row max
@@ -332,6 +335,8 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off 
     l.LPW = bank_place(o, &dslots);  o = l.LPW + 8 * l.lst_r;
     l.LANG = bank_place(o, &dslots); o = l.LANG + 8 * l.lst_r;
     l.CLA = round16(o);              o = l.CLA + 16 * (c > 0 ? c : 1);
+    l.NZ = o;                        o += 16 * (c > 0 ? c : 1);
+    l.PRE = o;                       o += round16(4 * (c > 0 ? c : 1));
     l.OFF = -1;
     if (with_off) {
         l.OFF = o;
