@@ -198,6 +198,9 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
         r.amax = rsa[i].angleMax;
         r.as = rsa[i].SourceIndex;
         r.at = rsa[i].TargetIndex;
+        // the two range normalisers, in the device's double arithmetic (no contraction)
+        r.norm_w = (mh::kTwoPI - (r.amax + (mh::kTwoPI - r.amin))) / 2.0;
+        r.norm_n = (mh::kTwoPI - (r.amax - r.amin)) / 2.0;
     }
     out.cfg0.resize((size_t)mh::F_COUNT * n);
     for (int i = 0; i < n; ++i) {

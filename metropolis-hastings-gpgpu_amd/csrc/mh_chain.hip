@@ -215,7 +215,28 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             sao[m] = comp_overlaps(rm, box);
         }
         rpw[m] = rang[m] = 0.0;
-        if (!(MH_ABLATE & 16) && i < rm.r) rel_terms(ch, i, rpw[m], rang[m]);
+        if (!(MH_ABLATE & 16) && i < rm.r) {
+            if constexpr (DELTA && NPL == 1) {
+                // a relationship whose objects did not move keeps its terms (the pass is
+                // skipped outright when a move touches no relationship)
+                const RelConst& rc = ch.relc[i];
+                const bool touched = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka ||
+                                                 rc.at == ka || rc.s == kb || rc.t == kb ||
+                                                 rc.as == kb || rc.at == kb);
+                if (touched) {
+                    rel_terms(ch, i, rpw[m], rang[m]);
+                } else {
+                    rpw[m] = clp.rpw;
+                    rang[m] = clp.rang;
+                }
+            } else {
+                rel_terms(ch, i, rpw[m], rang[m]);
+            }
+        }
+        if constexpr (NPL == 1) {
+            clo.rpw = rpw[0];
+            clo.rang = rang[0];
+        }
         if (i < c) {
             const RectShape cs = ch.clrs[i];
             const ObjP ps = ch.P[cs.pad];

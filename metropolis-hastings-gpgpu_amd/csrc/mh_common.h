@@ -497,6 +497,7 @@ struct SymRows {
 struct ClPairs {
     uint64_t cm;
     int buf;
+    double rpw, rang;  // this lane's relationship terms (kept for relationships a move misses)
 };
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
@@ -506,23 +507,25 @@ __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, dou
     tang = 0.0;
     const ObjP ps = P[rc.s], pt = P[rc.t];
     const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
-    if (d < rc.start) {
-        double f = d / rc.start;
-        tpw = f * f;
-    } else if (d > rc.end) {
-        double f = rc.end / d;
+    // d / start below the range, end / d above it: one division for either side
+    const bool below = d < rc.start, above = d > rc.end;
+    if (below || above) {
+        const double f = (below ? d : rc.end) / (below ? rc.start : d);
         tpw = f * f;
     }
     const ObjP as = P[rc.as], at = P[rc.at];
     const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
+    bool on;
+    double norm;
     if (rc.amin > rc.amax) {
-        double norm = (kTwoPI - (rc.amax + (kTwoPI - rc.amin))) / 2.0;
         float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
-        if ((double)w > rc.amax) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
-    } else if (rc.amin < th || th < rc.amax) {
-        double norm = (kTwoPI - (rc.amax - rc.amin)) / 2.0;
-        tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+        on = (double)w > rc.amax;
+        norm = rc.norm_w;
+    } else {
+        on = rc.amin < th || th < rc.amax;
+        norm = rc.norm_n;
     }
+    if (on) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
 }
 
 // ---- proposal draws and the accept rule ----------------------------------------------------

@@ -52,6 +52,8 @@ struct RelConst {   // relationship i: rss[i] and rsa[i] (sized by nRelationship
     double amin, amax;  // rsa[i].angleMin / angleMax
     int s, t;           // rss[i] Source / Target
     int as, at;         // rsa[i] Source / Target
+    double norm_w;      // (2PI - (amax + (2PI - amin))) / 2, Kernel.cu:247 (wrapped range)
+    double norm_n;      // (2PI - (amax - amin)) / 2, Kernel.cu:255 (plain range)
 };
 
 // Scalars of one room, passed by value as a kernel argument.

@@ -7,7 +7,7 @@ import glob
 import os
 from collections import defaultdict
 
-NAMES = {"dbl1": "A per-object", "dbl2": "B full symmetry", "dbl64": "B delta symmetry",
+NAMES = {"2": "ablate per-object atan2/cos", "16": "ablate PW/ANG terms", "dbl1": "A per-object", "dbl2": "B full symmetry", "dbl64": "B delta symmetry",
          "dbl4": "D surface area", "dbl8": "E clearance", "dbl16": "F pairwise appends",
          "dbl32": "G replay"}
 
@@ -35,16 +35,18 @@ def main():
     base = load(os.path.join(a.tag_dir, "pmc_0"), a.kernel)
     keys = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
             "SQ_ACTIVE_INST_VALU", "ns"]
-    hdr = f"{'phase':22s}" + "".join(f"{k.replace('SQ_INSTS_', '').replace('SQ_ACTIVE_INST_', 'act_'):>11s}" for k in keys)
+    hdr = f"{'phase':28s}" + "".join(f"{k.replace('SQ_INSTS_', '').replace('SQ_ACTIVE_INST_', 'act_'):>11s}" for k in keys)
     print(hdr)
-    print(f"{'whole step':22s}" + "".join(f"{base[k] / (steps if k != 'ns' else 1):11.1f}" for k in keys))
-    for d in sorted(glob.glob(os.path.join(a.tag_dir, "pmc_dbl*"))):
-        if not os.path.isdir(d):
-            continue
+    print(f"{'whole step':28s}" + "".join(f"{base[k] / (steps if k != 'ns' else 1):11.1f}" for k in keys))
+    # probe builds (dblK: phase run twice, +cost) and ablations (K: phase compiled out, -cost)
+    for d in sorted(glob.glob(os.path.join(a.tag_dir, "pmc_*"))):
         v = os.path.basename(d)[4:]
+        if not os.path.isdir(d) or v == "0":
+            continue
         c = load(d, a.kernel)
-        print(f"{NAMES.get(v, v):22s}" + "".join(
-            f"{(c[k] - base[k]) / (steps if k != 'ns' else 1):11.1f}" for k in keys))
+        sign = 1.0 if v.startswith("dbl") else -1.0
+        print(f"{NAMES.get(v, v):28s}" + "".join(
+            f"{sign * (c[k] - base[k]) / (steps if k != 'ns' else 1):11.1f}" for k in keys))
 
 
 if __name__ == "__main__":
