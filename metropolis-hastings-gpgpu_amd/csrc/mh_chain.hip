@@ -193,8 +193,9 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             // VisualBalanceCosts products, Kernel.cu:200-201.
             px[m] = (double)area * x;
             py[m] = (double)area * y;
-            // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188.
-            if (!(MH_ABLATE & 2)) {
+            // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
+            // object per lane: below, sharing the relationship terms' atan2 pass).
+            if (!(MH_ABLATE & 2) && !(DELTA && NPL == 1)) {
                 float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
                 float b = at - p.rotYf;
                 float ph = (float)((double)b + kHalfPI);
@@ -215,27 +216,48 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             sao[m] = comp_overlaps(rm, box);
         }
         rpw[m] = rang[m] = 0.0;
-        if (!(MH_ABLATE & 16) && i < rm.r) {
-            if constexpr (DELTA && NPL == 1) {
-                // a relationship whose objects did not move keeps its terms (the pass is
-                // skipped outright when a move touches no relationship)
+        if constexpr (DELTA && NPL == 1) {
+            // Steps, one object per lane: only the moved objects' FocalPoint terms and the
+            // relationships they touch change; the rest keep their terms. Both need an atan2
+            // (phi, Kernel.cu:187; theta, :175): one shared pass serves a lane's relationship
+            // or, failing that, its object; a lane that needs both takes a second (rare) pass.
+            const bool obj = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
+            bool rel = false;
+            if (i < rm.r && !(MH_ABLATE & 16)) {
                 const RelConst& rc = ch.relc[i];
-                const bool touched = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka ||
-                                                 rc.at == ka || rc.s == kb || rc.t == kb ||
-                                                 rc.as == kb || rc.at == kb);
-                if (touched) {
-                    rel_terms(ch, i, rpw[m], rang[m]);
-                } else {
-                    rpw[m] = clp.rpw;
-                    rang[m] = clp.rang;
-                }
-            } else {
-                rel_terms(ch, i, rpw[m], rang[m]);
+                rel = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka || rc.at == ka ||
+                                  rc.s == kb || rc.t == kb || rc.as == kb || rc.at == kb);
             }
+            const ObjP p = ch.P[i < n ? i : 0];
+            const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
+            double dy = fy, dx = fx, tpw = 0.0;
+            float ti = 0.0f;
+            if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
+            double a1 = 0.0, a2 = 0.0;
+            if (rel || obj) a1 = atan2(dy, dx);
+            if (rel && obj) a2 = atan2(fy, fx);
+            if (obj) {
+                float at = (float)(rel ? a2 : a1);
+                float b = at - p.rotYf;
+                float ph = (float)((double)b + kHalfPI);
+                cph[m] = cos_f32(ph);
+            } else {
+                cph[m] = clp.cph;
+            }
+            if (rel) {
+                rpw[m] = tpw;
+                rang[m] = rel_angle(ch.relc[i], a1, ti);
+            } else {
+                rpw[m] = clp.rpw;
+                rang[m] = clp.rang;
+            }
+        } else if (!(MH_ABLATE & 16) && i < rm.r) {
+            rel_terms(ch, i, rpw[m], rang[m]);
         }
         if constexpr (NPL == 1) {
             clo.rpw = rpw[0];
             clo.rang = rang[0];
+            clo.cph = cph[0];
         }
         if (i < c) {
             const RectShape cs = ch.clrs[i];

@@ -498,9 +498,47 @@ struct ClPairs {
     uint64_t cm;
     int buf;
     double rpw, rang;  // this lane's relationship terms (kept for relationships a move misses)
+    float cph;         // this lane's object's cos(phi) (kept for objects a move misses)
 };
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
+// Split form for callers that batch the atan2: rel_pair() gives the PairWise term and theta's
+// atan2 arguments (and the target's rotation), rel_angle() the angle term from that atan2.
+__device__ __forceinline__ double rel_pair(const RelConst& rc, const ObjP* P, double& dy,
+                                           double& dx, float& ti) {
+    double tpw = 0.0;
+    const ObjP ps = P[rc.s], pt = P[rc.t];
+    const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
+    // d / start below the range, end / d above it: one division for either side
+    const bool below = d < rc.start, above = d > rc.end;
+    if (below || above) {
+        const double f = (below ? d : rc.end) / (below ? rc.start : d);
+        tpw = f * f;
+    }
+    const ObjP as = P[rc.as], at = P[rc.at];
+    dx = (double)(float)(as.xf - at.xf);  // theta(), Kernel.cu:170-182
+    dy = (double)(float)(as.yf - at.yf);
+    ti = at.rotYf;
+    return tpw;
+}
+
+__device__ __forceinline__ double rel_angle(const RelConst& rc, double tp, float ti) {
+    if (tp < 0) tp = kTwoPI + tp;
+    const double t = tp - (double)ti;
+    const double th = (t < 0) ? kTwoPI + t : t;
+    bool on;
+    double norm;
+    if (rc.amin > rc.amax) {
+        float w = fmodf((float)(rc.amin + th), (float)kTwoPI);
+        on = (double)w > rc.amax;
+        norm = rc.norm_w;
+    } else {
+        on = rc.amin < th || th < rc.amax;
+        norm = rc.norm_n;
+    }
+    return on ? fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm : 0.0;
+}
+
 __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, double& tpw,
                                           double& tang) {
     tpw = 0.0;
