@@ -270,11 +270,18 @@ bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
         max_lds = 64 * 1024;
-    // Four waves per workgroup while that keeps at least two workgroups per CU.
+    // Four waves per workgroup (one per SIMD) while that keeps at least two workgroups per CU.
+    // Measured at N = 64 (chain-steps/s by waves per workgroup): 2: 2.70e8, 3: 2.84e8,
+    // 4: 2.96e8, 5: 2.83e8, 8: 2.84e8 -- the runtime's occupancy optimum (7, more resident
+    // chains) measured 2.50e8. $MH_WAVES (1..8) pins it for experiments.
     g.waves = 4;
     while (g.waves > 1 && mh::lds_bytes(g.lay, g.L, g.waves) > 80 * 1024) g.waves >>= 1;
+    if (const char* e = getenv("MH_WAVES")) {
+        const int w = atoi(e);
+        if (w >= 1 && w <= 8 && mh::lds_bytes(g.lay, g.L, w) <= (size_t)max_lds) g.waves = w;
+    }
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
-    g.waves_ol = g.waves;
+    g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
     if (mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > (size_t)max_lds) {
         set_error("room does not fit in LDS");

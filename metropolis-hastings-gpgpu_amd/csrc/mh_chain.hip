@@ -73,8 +73,8 @@ struct ChainPtrs {
     ObjP* P;
     double* RY;
     double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
-    float *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max)
-    float* LCL;       // compacted non-zero Clearance terms (floats), capacity 2L
+    double *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
+    double* LCL;      // compacted non-zero Clearance terms (float values), capacity 2L
     double* LPW;      // compacted non-zero PairWise / Angle terms, capacity lst_r each
     double* LANG;
     int lst_r;
@@ -86,6 +86,7 @@ struct ChainPtrs {
     int* PRE;         // [C] row prefix counts
     ChainAux* aux;
     const DevRoom* rm;  // LDS copy of the room scalars
+    const double* zero4;  // four zero doubles (a finished replay lane reads these)
 };
 
 // ---- compacted term lists for the ordered sums -------------------------------------------
@@ -608,7 +609,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                     const int i = __builtin_ctzll(bits);
                     bits &= bits - 1;
                     const int pos = ch.PRE[i] + __builtin_popcountll(NZn[i] & below);
-                    ch.LCL[pos] = -overlap(ch.CLA[i], boxj);
+                    ch.LCL[pos] = (double)-overlap(ch.CLA[i], boxj);
                 }
                 cnt_cl = total;
                 cl_done = true;
@@ -651,20 +652,20 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         const float4 A0 = A0n, A1 = A1n;
         if (ci + 2 < cend) A0n = ch.CLA[ci + 2];
         if (ci + 3 < cend) A1n = ch.CLA[ci + 3];
-        float v[2 * NPL];
+        double v[2 * NPL];
         bool nz[2 * NPL];
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
             const bool own = m * L + r < n;
             const float a0 = own ? overlap(A0, offb[m]) : 0.0f;
             const float a1 = own ? overlap(A1, offb[m]) : 0.0f;
-            v[m] = -a0;
+            v[m] = (double)-a0;
             nz[m] = a0 != 0.0f;
-            v[NPL + m] = -a1;
+            v[NPL + m] = (double)-a1;
             nz[NPL + m] = a1 != 0.0f;
         }
-        list_append_n<L, 2 * NPL, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, v, nz, r,
-                                         gbase);
+        list_append_n<L, 2 * NPL, double>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, v, nz, r,
+                                          gbase);
     }
     for (; ci < cend; ++ci) {
         const float4 A = A0n;  // box ci; box ci + 1 is in flight during the appends
@@ -673,8 +674,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         for (int m = 0; m < NPL; ++m) {
             const int j = m * L + r;
             const float ar = (j < n) ? overlap(A, offb[m]) : 0.0f;
-            list_append<L, float>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, -ar, ar != 0.0f, r,
-                                  gbase);
+            list_append<L, double>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, (double)-ar,
+                                   ar != 0.0f, r, gbase);
         }
     }
     }
@@ -710,7 +711,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // 6/7: PairWise / Angle lists (double, double). Every sequence is zero-padded to a multiple
     // of four terms; a lane reads four at a time (two ds_read_b128 of doubles or one of
     // floats) and keeps both a double- and a float-rounded walk of the same terms.
-    for (int q = cnt_cl + r; q < ((cnt_cl + 3) & ~3); q += L) ch.LCL[q] = 0.0f;
+    for (int q = cnt_cl + r; q < ((cnt_cl + 3) & ~3); q += L) ch.LCL[q] = 0.0;
     for (int q = cnt_pw + r; q < ((cnt_pw + 3) & ~3); q += L) ch.LPW[q] = 0.0;
     for (int q = cnt_ang + r; q < ((cnt_ang + 3) & ~3); q += L) ch.LANG[q] = 0.0;
     wave_sync();
@@ -718,18 +719,16 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     for (int rep = 0; rep < MH_REPS(32); ++rep) {
         MH_CLOBBER();
         const int k = r;
-        const double* dsrc = ch.PX;
-        const float* fsrc = ch.CPHF;
+        const double* dsrc = ch.zero4;
         int len = 0;
-        const bool is_d = (k == 0 || k == 1 || k == 6 || k == 7);
         if (k == 0 || k == 1) {
             dsrc = k == 0 ? ch.PX : ch.PY;
             len = n;
         } else if (k == 2 || k == 3) {
-            fsrc = k == 2 ? ch.CPHF : ch.RMXF;
+            dsrc = k == 2 ? ch.CPHF : ch.RMXF;
             len = n;
         } else if (k == 4) {
-            fsrc = ch.LCL;
+            dsrc = ch.LCL;
             len = cnt_cl;
         } else if (k == 6 || k == 7) {
             dsrc = k == 6 ? ch.LPW : ch.LANG;
@@ -742,23 +741,11 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         const int steps = group_max<L>(len_main);
         double accd = acc0, accf = acc0;
         for (int l0 = 0; l0 < steps; l0 += 4) {
-            double v[4] = {0.0, 0.0, 0.0, 0.0};
-            if (l0 < len) {
-                if (is_d) {
-                    const double2 a0 = *reinterpret_cast<const double2*>(dsrc + l0);
-                    const double2 a1 = *reinterpret_cast<const double2*>(dsrc + l0 + 2);
-                    v[0] = a0.x;
-                    v[1] = a0.y;
-                    v[2] = a1.x;
-                    v[3] = a1.y;
-                } else {
-                    const float4 f = *reinterpret_cast<const float4*>(fsrc + l0);
-                    v[0] = f.x;
-                    v[1] = f.y;
-                    v[2] = f.z;
-                    v[3] = f.w;
-                }
-            }
+            // every stream holds doubles; a lane past its end reads four zeros
+            const double* src = l0 < len ? dsrc + l0 : ch.zero4;
+            const double2 a0 = *reinterpret_cast<const double2*>(src);
+            const double2 a1 = *reinterpret_cast<const double2*>(src + 2);
+            const double v[4] = {a0.x, a0.y, a1.x, a1.y};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 accd = accd + v[u];
@@ -768,11 +755,12 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         if (k == 4 && len > steps) {
             float a32 = (float)accf;
             for (int l0 = steps; l0 < len; l0 += 4) {
-                const float4 f = *reinterpret_cast<const float4*>(fsrc + l0);
-                a32 = a32 + f.x;
-                a32 = a32 + f.y;
-                a32 = a32 + f.z;
-                a32 = a32 + f.w;
+                const double2 a0 = *reinterpret_cast<const double2*>(dsrc + l0);
+                const double2 a1 = *reinterpret_cast<const double2*>(dsrc + l0 + 2);
+                a32 = a32 + (float)a0.x;
+                a32 = a32 + (float)a0.y;
+                a32 = a32 + (float)a1.x;
+                a32 = a32 + (float)a1.y;
             }
             accf = a32;
         }
@@ -951,7 +939,7 @@ __device__ __forceinline__ int64_t out_index(const LaunchArgs& a, int64_t chain)
 }
 
 template <int L, int NPL, int OP>
-__global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
+__global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // OP_STEP_T: OP_STEP with best-of-chain tracking compiled in; OP_STEP_XW: the same drawing
     // from the cuRAND XORWOW stream instead of Philox. Plain OP_STEP carries no tracking code.
@@ -987,6 +975,7 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + F.h_room);
     if (threadIdx.x == 0) *rm_l = a.rm;
+    if (threadIdx.x < 4) reinterpret_cast<double*>(lds + F.h_zero)[threadIdx.x] = 0.0;
     __syncthreads();
 
     const int64_t chain = ((int64_t)blockIdx.x * waves_per_wg + wave) * G + g;
@@ -1001,9 +990,9 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.RY = reinterpret_cast<double*>(base + F.RY);
     ch.PX = reinterpret_cast<double*>(base + F.PX);
     ch.PY = reinterpret_cast<double*>(base + F.PY);
-    ch.CPHF = reinterpret_cast<float*>(base + F.CPHF);
-    ch.RMXF = reinterpret_cast<float*>(base + F.RMXF);
-    ch.LCL = reinterpret_cast<float*>(base + F.LCL);
+    ch.CPHF = reinterpret_cast<double*>(base + F.CPHF);
+    ch.RMXF = reinterpret_cast<double*>(base + F.RMXF);
+    ch.LCL = reinterpret_cast<double*>(base + F.LCL);
     ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
     ch.lst_r = a.lay.lst_r;
     ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
@@ -1016,13 +1005,14 @@ __global__ void __launch_bounds__(256) MH_OCC mh_kernel(LaunchArgs a) {
     ch.PRE = reinterpret_cast<int*>(base + a.lay.PRE);
     ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
+    ch.zero4 = reinterpret_cast<const double*>(lds + F.h_zero);
 
     // Zero the dense replay streams past N (never written afterwards).
     for (int i = n + r; i < a.lay.N4; i += L) {
         ch.PX[i] = 0.0;
         ch.PY[i] = 0.0;
-        ch.CPHF[i] = 0.0f;
-        ch.RMXF[i] = 0.0f;
+        ch.CPHF[i] = 0.0;
+        ch.RMXF[i] = 0.0;
     }
     // Stage the configuration into LDS.
     const double* src;

@@ -275,7 +275,7 @@ inline MH_HD constexpr int bank_place_c(int o, unsigned& used) {
 // the workgroup with the same function. Header: DevRoom, object shapes, frozen flags, then the
 // clearance shapes; the relationship table follows at a run-time offset.
 struct FixedLds {
-    int h_room, h_obj, h_frz, h_clr;                    // workgroup header
+    int h_room, h_obj, h_frz, h_zero, h_clr;            // workgroup header (h_zero: 4 zero doubles)
     int P, RY, X, Y, AUX, PX, PY, CPHF, RMXF, LCL, end;  // per chain
 };
 
@@ -285,21 +285,23 @@ inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
     f.h_room = 0;
     f.h_obj = round16c((int)sizeof(DevRoom));
     f.h_frz = f.h_obj + round16c((int)sizeof(RectShape) * NC);
-    f.h_clr = f.h_frz + round16c(NC + 1);
+    f.h_zero = f.h_frz + round16c(NC + 1);
+    f.h_clr = f.h_zero + 32;
     int o = 0;
     f.P = o;   o += 16 * NC;
     f.RY = o;  o += 8 * NC;
     f.X = o;   o += 8 * NC;
     f.Y = o;   o += 8 * NC;
     f.AUX = o; o += kChainAuxBytes;
-    // The replay's streams: lanes 0, 1, 6, 7 read PX, PY, LPW, LANG with one instruction,
-    // lanes 2, 3, 4 read CPHF, RMXF, LCL with another -- each set on distinct banks.
-    unsigned dslots = 0u, fslots = 0u;
+    // The replay's streams, all doubles (float terms are widened when written, one instruction
+    // for all lanes, instead of inside the serial walk): lanes 0..4, 6, 7 read PX, PY, CPHF,
+    // RMXF, LCL, LPW, LANG with one instruction, each stream starting on its own banks.
+    unsigned dslots = 0u;
     f.PX = bank_place_c(o, dslots);   o = f.PX + 8 * NC;
     f.PY = bank_place_c(o, dslots);   o = f.PY + 8 * NC;
-    f.CPHF = bank_place_c(o, fslots); o = f.CPHF + 4 * NC;
-    f.RMXF = bank_place_c(o, fslots); o = f.RMXF + 4 * NC;
-    f.LCL = bank_place_c(o, fslots);  o = f.LCL + 8 * L;
+    f.CPHF = bank_place_c(o, dslots); o = f.CPHF + 8 * NC;
+    f.RMXF = bank_place_c(o, dslots); o = f.RMXF + 8 * NC;
+    f.LCL = bank_place_c(o, dslots);  o = f.LCL + 16 * L;
     f.end = o;
     return f;
 }
@@ -331,9 +333,12 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off 
     l.lst_r = ((r < 1 ? 1 : (r < L ? r : L)) + 3) & ~3;
     l.N4 = (n + 3) & ~3;
     int o = f.end;
-    unsigned dslots = 0u;  // LPW / LANG on banks apart from PX / PY
+    unsigned dslots = 0u;  // LPW / LANG on banks apart from the other replay streams
     dslots |= 1u << ((f.PX >> 4) & 15);
     dslots |= 1u << ((f.PY >> 4) & 15);
+    dslots |= 1u << ((f.CPHF >> 4) & 15);
+    dslots |= 1u << ((f.RMXF >> 4) & 15);
+    dslots |= 1u << ((f.LCL >> 4) & 15);
     l.LPW = bank_place(o, &dslots);  o = l.LPW + 8 * l.lst_r;
     l.LANG = bank_place(o, &dslots); o = l.LANG + 8 * l.lst_r;
     l.CLA = round16(o);              o = l.CLA + 16 * (c > 0 ? c : 1);
