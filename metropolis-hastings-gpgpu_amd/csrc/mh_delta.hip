@@ -677,7 +677,11 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     if (((int64_t)blockIdx.x * waves_per_wg + wave) * G >= a.n_chains) return;
     const bool live = chain < a.n_chains;
 
-    unsigned char* base = lds + lay.hdr + (wave * G + g) * lay.stride;
+    // The per-chain LDS addresses are computed into VGPRs (an opaque v_mov), not kept in SGPRs:
+    // this kernel is bound by LDS per chain, not registers, and the scalar file was spilling.
+    int boff = lay.hdr + (wave * G + g) * lay.stride;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(boff) : "v"(boff));
+    unsigned char* base = lds + boff;
     DeltaPtrs ch;
     ch.objc = objc_l;
     ch.clrc = clrc_l;
@@ -744,7 +748,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     wave_sync();
     int wild = 0;
     for (int i = r; i < n; i += L) {
-        ch.CPH[i] = -focal_cos(a.rm, ch.P[i]);
+        ch.CPH[i] = -focal_cos(*rm_l, ch.P[i]);
         wild += wild_pose(ch.X[i], ch.Y[i], ch.RY[i]) ? 1 : 0;
     }
     int wild_cnt = group_sum<L>(wild);
@@ -781,7 +785,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
 #pragma clang loop unroll(disable)
     for (int it = 0; it < a.iterations; ++it) {
         for (int w = r; w < ch.SW; w += L) ch.SAMB[w] = ch.SAM[w];
-        const int2 kk = propose(rng, a.rm, frozen, ch, writer);
+        const int2 kk = propose(rng, *rm_l, frozen, ch, writer);
         const int ka = kk.x, kb = kk.y;
         wave_sync();
         // Objects ka (lane 0) and kb (lane 1): FocalPoint term, SurfaceArea bits, wildness.
@@ -790,10 +794,10 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
             const int k = r == 0 ? ka : kb;
             if (k >= 0) {
                 const ObjP p = ch.P[k];
-                ch.CPH[k] = -focal_cos(a.rm, p);
-                sam_put(ch, c + k, nonzero4(comp_overlaps(a.rm, shape_box(ch.objc[k].off, p.xf, p.yf))));
+                ch.CPH[k] = -focal_cos(*rm_l, p);
+                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.objc[k].off, p.xf, p.yf))));
                 if (k < c)
-                    sam_put(ch, k, nonzero4(comp_overlaps(a.rm, shape_box(ch.clrc[k].shape, p.xf, p.yf))));
+                    sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrc[k].shape, p.xf, p.yf))));
                 const DBackup& ob = ch.aux->b[r];
                 dwild = (wild_pose(ch.X[k], ch.Y[k], ch.RY[k]) ? 1 : 0) -
                         (wild_pose(ob.x, ob.y, ob.ry) ? 1 : 0);
