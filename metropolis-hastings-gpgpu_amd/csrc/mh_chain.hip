@@ -171,7 +171,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
 
     unsigned long long t0 = 0;
     MH_STAMP(t0);
-    // Phase A: per-object and per-clearance terms of the owned slots.
+    // Phase A: per-object and per-clearance terms of the owned slots. Steps with one object per
+    // lane keep terms across steps and share one atan2 pass (below); the 8-lane instance (rooms
+    // of up to 8 objects: latency-bound, few chains) keeps the direct per-lane passes.
+    constexpr bool SHARED = DELTA && NPL == 1 && L >= 16;
     double px[NPL], py[NPL];
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
@@ -196,7 +199,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             py[m] = (double)area * y;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
             // object per lane: below, sharing the relationship terms' atan2 pass).
-            if (!(MH_ABLATE & 2) && !(DELTA && NPL == 1)) {
+            if (!(MH_ABLATE & 2) && !SHARED) {
                 float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
                 float b = at - p.rotYf;
                 float ph = (float)((double)b + kHalfPI);
@@ -217,7 +220,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             sao[m] = comp_overlaps(rm, box);
         }
         rpw[m] = rang[m] = 0.0;
-        if constexpr (DELTA && NPL == 1) {
+        if constexpr (SHARED) {
             // Steps, one object per lane: only the moved objects' FocalPoint terms and the
             // relationships they touch change; the rest keep their terms. Both need an atan2
             // (phi, Kernel.cu:187; theta, :175): one shared pass serves a lane's relationship
@@ -561,7 +564,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // others keep their zero / non-zero state, so only the non-zero pairs are re-evaluated,
     // each by its object's lane, and written straight to their list positions (row prefix +
     // the row's set bits below the object).
-    constexpr bool INC_CL = DELTA && NPL == 1;
+    // (The 8-lane instance keeps the direct pass: with a handful of clearances its latency is
+    // lower, and those rooms run few chains -- config 2 is latency-bound.)
+    constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
+    constexpr bool CL_STATE = NPL == 1 && L >= 16;  // pair state kept for the steps
     bool cl_done = false;
     if constexpr (NPL == 1) {
         const int j = r;
@@ -614,7 +620,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 cnt_cl = total;
                 cl_done = true;
             }
-        } else {
+        } else if constexpr (!DELTA && CL_STATE) {
             // full evaluation: the pair state from scratch, for the steps that follow
             uint64_t cm = 0ull;
             for (int i = 0; i < c; ++i) {
