@@ -951,7 +951,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     // from the cuRAND XORWOW stream instead of Philox. Plain OP_STEP carries no tracking code.
     constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_T || OP == OP_STEP_XW);
     constexpr bool TRACK = (OP == OP_STEP_T || OP == OP_STEP_XW);
-    using Rng = typename RngOf<OP == OP_STEP_XW>::type;
+    using Rng = typename RngOf<OP == OP_STEP_XW, L>::type;
     constexpr int G = 64 / L;
     const int n = a.rm.n;
     const int lane = threadIdx.x & 63;
@@ -1084,6 +1084,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         for (int it = 0; it < a.iterations; ++it) {
             unsigned long long ts = 0;
             MH_STAMP(ts);
+            rng_prepare(rng);
             const int2 kk = propose(rng, *rm_l, frozen, ch, writer);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);

@@ -70,7 +70,7 @@ __device__ __forceinline__ double grp_get(double v, int src, int gbase) {
 
 // Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
 // OCML log/sin/cos code is not duplicated at every call site.
-static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
+__device__ __forceinline__ float2 box_muller_inl(unsigned int a, unsigned int b) {
     if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
     const double u1 = (double)a * 0x1p-32 + 0x1p-33;
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
@@ -79,6 +79,11 @@ static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, un
     double s, c;
     sincos(ang, &s, &c);  // OCML's sin and cos share one argument reduction
     return make_float2((float)(rad * s), (float)(rad * c));
+}
+
+// Out of line so its OCML log/sin/cos code is not duplicated at every call site.
+static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
+    return box_muller_inl(a, b);
 }
 
 // rocRAND Philox4x32-10 stream of one chain. Words are taken a block of four at a time with
@@ -185,8 +190,97 @@ struct ChainRngXw {
     }
 };
 
-template <bool XW> struct RngOf { using type = ChainRng; };
-template <> struct RngOf<true> { using type = ChainRngXw; };
+// The Philox stream of a chain that owns a whole wavefront (L = 64), drawn 64 words at a
+// time: lane i holds word base + i and the Box-Muller pair of words (base + i, base + i + 1),
+// so one pass of the double log / sincos serves every normal drawn from the window instead of
+// one pass per normal. Draws read the window with v_readlane at the (uniform) draw index. The
+// words and normals are exactly ChainRng's.
+struct WaveWindow {
+    unsigned int w;
+    float bs, bc;
+};
+
+// Word d of a Philox stream: its block by rocrand4 (as ChainRng draws it) and the word picked
+// without dynamic register indexing (that went through scratch).
+__device__ __forceinline__ unsigned int philox_word(uint64_t seed, uint64_t subseq, uint64_t d) {
+    rocrand_state_philox4x32_10 st;
+    rocrand_init(seed, subseq, d & ~3ull, &st);
+    const uint4 b = rocrand4(&st);
+    const int q = (int)(d & 3);
+    return q == 0 ? b.x : q == 1 ? b.y : q == 2 ? b.z : b.w;
+}
+
+// One window of WaveRng: lane i's word base + i and its Box-Muller pair.
+__device__ __forceinline__ WaveWindow wave_window(uint64_t seed, uint64_t subseq, uint64_t at) {
+    const int lane = __lane_id();
+    WaveWindow ww;
+    ww.w = philox_word(seed, subseq, at + (uint64_t)lane);
+    const unsigned int w1 = (unsigned int)__shfl_down((int)ww.w, 1);  // lane 63's is unused
+    const float2 z = box_muller_inl(ww.w, w1);
+    ww.bs = z.x;
+    ww.bc = z.y;
+    return ww;
+}
+
+struct WaveRng {
+    uint64_t seed, subseq;
+    uint64_t base;   // first draw of the window
+    uint64_t draws;  // next draw
+    unsigned int w;  // lane i: word base + i
+    float bs, bc;    // lane i: box_muller(word base + i, word base + i + 1)
+    int bm_has;
+    float bm_val;
+
+    __device__ __forceinline__ void fill(uint64_t at) {
+        base = at;
+        const WaveWindow ww = wave_window(seed, subseq, at);
+        w = ww.w;
+        bs = ww.bs;
+        bc = ww.bc;
+    }
+    // Called once per step (the only place a window is filled): starts a new window unless 16
+    // draws remain in this one. A step that runs past the window (long frozen-object redraw
+    // runs) draws the word directly instead.
+    __device__ __forceinline__ void prepare() {
+        if (draws - base > 64 - 16) fill(draws);
+    }
+    __device__ __forceinline__ unsigned int word_at(uint64_t d) const {
+        if (d - base < 64) return (unsigned int)__builtin_amdgcn_readlane((int)w, (int)(d - base));
+        return philox_word(seed, subseq, d);
+    }
+    __device__ __forceinline__ unsigned int next() { return word_at(draws++); }
+    __device__ __forceinline__ float uniform() {
+        return rocrand_device::detail::uniform_distribution(next());
+    }
+    __device__ __forceinline__ float normal() {
+        if (bm_has) {
+            bm_has = 0;
+            return bm_val;
+        }
+        float zs, zc;
+        if (draws - base < 63) {
+            const int i = (int)(draws - base);
+            zs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), i));
+            zc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bc), i));
+        } else {
+            // (inline: an out-of-line call here made the kernel spill across it)
+            const float2 z = box_muller_inl(word_at(draws), word_at(draws + 1));
+            zs = z.x;
+            zc = z.y;
+        }
+        draws += 2;
+        bm_val = zc;
+        bm_has = 1;
+        return zs;
+    }
+};
+
+template <bool XW, int L = 0> struct RngOf { using type = ChainRng; };
+template <> struct RngOf<false, 64> { using type = WaveRng; };
+template <int L> struct RngOf<true, L> { using type = ChainRngXw; };
+
+template <class R> __device__ __forceinline__ void rng_prepare(R&) {}
+__device__ __forceinline__ void rng_prepare(WaveRng& r) { r.prepare(); }
 
 // Resume / save a chain's stream around a launch. Philox resumes from the draw count; XORWOW
 // from its saved state words.
@@ -209,6 +303,16 @@ __device__ __forceinline__ void rng_load(ChainRngXw& r, const LaunchArgs& a, int
     r.bm_has = m.bm_has;
     r.bm_val = m.bm_val;
 }
+__device__ __forceinline__ void rng_load(WaveRng& r, const LaunchArgs& a, int64_t chain,
+                                         const ChainMeta& m) {
+    r.seed = a.seed;
+    r.subseq = (uint64_t)(a.chain_offset + chain);
+    r.draws = m.draws;
+    r.bm_has = m.bm_has;
+    r.bm_val = m.bm_val;
+    r.fill(m.draws);
+}
+__device__ __forceinline__ void rng_save(const WaveRng&, const LaunchArgs&, int64_t) {}
 __device__ __forceinline__ void rng_save(const ChainRng&, const LaunchArgs&, int64_t) {}
 __device__ __forceinline__ void rng_save(const ChainRngXw& r, const LaunchArgs& a, int64_t chain) {
     unsigned int* w = a.xw + chain * 6;
