@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     float cur_total = m0.costs[0];
     if (writer)
         for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
-    typename RngOf<XW>::type rng;
+    typename RngOf<XW, L>::type rng;
     rng_load(rng, a, cidx, m0);
     uint64_t accepted = m0.accepted;
     float best_total = m0.best_total;
@@ -785,6 +785,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
 #pragma clang loop unroll(disable)
     for (int it = 0; it < a.iterations; ++it) {
         for (int w = r; w < ch.SW; w += L) ch.SAMB[w] = ch.SAM[w];
+        rng_prepare(rng);
         const int2 kk = propose(rng, *rm_l, frozen, ch, writer);
         const int ka = kk.x, kb = kk.y;
         wave_sync();
