@@ -688,19 +688,27 @@ __device__ __forceinline__ int pick_object(Rng& rng, int n, const unsigned char*
 }
 
 // Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
+// The threshold min(1, (float)exp(x)) of Accept without evaluating exp where it is decided:
+// x >= 0 gives exp(x) >= 1, so the threshold is exactly 1; x < -24 gives (float)exp(x) <
+// 3.8e-11, below every uniform either stream draws (>= 2^-33), so any u rejects -- 0 decides
+// the same. (The uniform is drawn in every case, so the stream is unchanged.)
+__device__ __forceinline__ float accept_threshold(double x) {
+    if (x >= 0.0) return 1.0f;
+    if (x < -24.0) return 0.0f;
+    return fminf(1.0f, (float)exp(x));
+}
+
 template <class Rng>
 __device__ __forceinline__ bool accept(Rng& rng, float star, float cur) {
     const float u = rng.uniform();
-    const float thr = fminf(1.0f, (float)exp(kBeta * ((double)star - (double)cur)));
-    return u < thr;
+    return u < accept_threshold(kBeta * ((double)star - (double)cur));
 }
 
 // The same at inverse temperature beta (parallel tempering; beta = kBeta is Accept itself).
 template <class Rng>
 __device__ __forceinline__ bool accept_at(Rng& rng, float star, float cur, double beta) {
     const float u = rng.uniform();
-    const float thr = fminf(1.0f, (float)exp(beta * ((double)star - (double)cur)));
-    return u < thr;
+    return u < accept_threshold(beta * ((double)star - (double)cur));
 }
 
 }  // namespace mh
