@@ -574,3 +574,24 @@ def test_tempering_validation(mh, hiplib):
         mh.kernel_wrapper(room, 10, 10, seed=1, temps=4, swap_interval=5, beta_min=0.5)
     with pytest.raises(mh.MHError, match="beta_min"):
         mh.kernel_wrapper(room, 8, 10, seed=1, temps=4, swap_interval=5, beta_min=3.0)
+
+
+@pytest.mark.parametrize("step", ["full", "incremental"])
+def test_wave_rng_window_overrun(mh, orc, hiplib, monkeypatch, step):
+    """A 64-object room with 61 objects frozen: a pick redraws ~20 times on average, so steps
+    regularly draw past WaveRng's 64-word window (the direct-draw fallback for words and
+    normals). Bit for bit against the oracle, including across launch boundaries."""
+    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    monkeypatch.setenv("MH_DELTA_LANES", "64")  # one chain per wavefront: the WaveRng instance
+    room = mh.synthetic_room(64)
+    for i in range(61):
+        room.cfg[i].frozen = True
+    chains, steps, seed = 64, 1300, 606
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel()[:1] == (64,) and s.step_kernel()[2] == step
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
+    assert np.array_equal(pts.view(np.uint32), ref_pts.view(np.uint32))
+    assert np.array_equal(costs.view(np.uint32), ref_costs.view(np.uint32))
