@@ -527,13 +527,18 @@ __device__ __forceinline__ void commit_swap_zrr(const DeltaPtrs& ch, int n) {
 // accumulator a, four at a time: the reference's float accumulator with float terms, so the
 // double-rounded add of the dense walk equals the plain fp32 add (53 >= 2 * 24 + 2 bits). The
 // entries up to round4(to) are zero (x + 0 == x).
+// The next four terms are loaded before the current four are added, so the LDS latency
+// overlaps the dependent adds (these walks run ~1,000 terms at N = 256 on few waves per SIMD).
 __device__ __forceinline__ float list_walk(const float* fs, int from, int to, float a) {
+    if (from >= to) return a;
+    float4 q = *reinterpret_cast<const float4*>(fs + from);
     for (int l = from; l < to; l += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(fs + l);
+        const float4 nq = (l + 4 < to) ? *reinterpret_cast<const float4*>(fs + l + 4) : q;
         a = a + q.x;
         a = a + q.y;
         a = a + q.z;
         a = a + q.w;
+        q = nq;
     }
     return a;
 }
