@@ -457,20 +457,19 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 tj = up ? j : tj;
             }
         }
-        group_top2<L>(t1, t2, tj);
+        const SymLead ld = group_sym_lead<L>(t1, t2, tj, r, gbase, rr);
         float best = 0.0f;
         int barg = -1;
-        const bool clear = !exact_mode && tj >= 0 &&
-                           (t2 == -INFINITY || t1 - t2 > sym_err(t1, rr) + sym_err(t2, rr));
+        const bool clear = !exact_mode && ld.clear;
         if (!clear) {
             const float thr =
-                (exact_mode || tj < 0) ? INFINITY : 2.0f * sym_err(fabsf(t1) + 1.0f, rr);
+                (exact_mode || ld.j < 0) ? INFINITY : 2.0f * sym_err(fabsf(ld.m) + 1.0f, rr);
             float bv = -INFINITY;
             int bj = -1;
             for (int j = r; j < n; j += L) {
                 const ObjP p = ch.P[j];
                 const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
-                if (!(v < t1 - thr)) {
+                if (!(v < ld.m - thr)) {
                     const float e = sym_val_exact(p.xf, p.yf, ch.RY[j], rx, ry, (double)rr);
                     if (e > bv) {
                         bv = e;
@@ -488,7 +487,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             if (m == ms) {
                 if (r == b) {
                     if (clear) {
-                        lead[m] = tj;
+                        lead[m] = ld.j;
                         leadp |= 1u << m;
                     } else {
                         sym.mx[m] = best;

@@ -507,6 +507,39 @@ __device__ __forceinline__ void group_top2(float& m1, float& m2, int& j1) {
     if constexpr (L >= 64) level(bfly<32>(m1), bfly<32>(m2), bfly<32>(j1));
 }
 
+// Leader of a screened symmetry row from each lane's best two estimates (t1 at column tj, t2):
+// the group maximum m, its column j, and whether it is clear -- held by one lane only, with
+// every other estimate more than the two error bounds below m. Each lane tests its runner-up
+// (t2 on the leader's lane, t1 elsewhere); its lower estimates are further away. One max
+// butterfly and two ballots, where a top-two reduction moves three values per level.
+struct SymLead {
+    float m;
+    int j;
+    bool clear;
+};
+
+template <int L>
+__device__ __forceinline__ SymLead group_sym_lead(float t1, float t2, int tj, int r, int gbase,
+                                                  float rr) {
+    float m = t1;
+    m = fmaxf(m, bfly<1>(m));
+    m = fmaxf(m, bfly<2>(m));
+    if constexpr (L >= 8) m = fmaxf(m, bfly<4>(m));
+    if constexpr (L >= 16) m = fmaxf(m, bfly<8>(m));
+    if constexpr (L >= 32) m = fmaxf(m, bfly<16>(m));
+    if constexpr (L >= 64) m = fmaxf(m, bfly<32>(m));
+    // t1 is never NaN (it only takes values that compare greater), so some lane holds m.
+    const uint64_t at = group_ballot<L>(t1 == m, gbase);
+    const int lb = __builtin_ctzll(at);
+    SymLead o;
+    o.m = m;
+    o.j = __float_as_int(grp_get<L>(__int_as_float(tj), lb, gbase));
+    const float other = r == lb ? t2 : t1;
+    const bool near = !(other == -INFINITY || m - other > sym_err(m, rr) + sym_err(other, rr));
+    o.clear = o.j >= 0 && (at & (at - 1)) == 0 && group_ballot<L>(near, gbase) == 0;
+    return o;
+}
+
 // Group-wide maximum of v with its index (ties: lowest index).
 template <int L>
 __device__ __forceinline__ void group_max_arg(float& v, int& j) {

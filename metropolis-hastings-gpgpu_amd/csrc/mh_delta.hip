@@ -152,7 +152,7 @@ __device__ __forceinline__ void sam_put(const DeltaPtrs& ch, int e, bool nz) {
 // estimates screen the pairs (sym_err bounds their error), the leader is evaluated exactly and
 // an ambiguous top two falls back to the exact value of every candidate within the bound.
 template <int L>
-__device__ RowMax scan_row(const DeltaPtrs& ch, int n, int i, bool exact_mode, int r) {
+__device__ RowMax scan_row(const DeltaPtrs& ch, int n, int i, bool exact_mode, int r, int gbase) {
     float rx, ry, rr;
     row_setup(ch, i, rx, ry, rr);
     float t1 = -INFINITY, t2 = -INFINITY;
@@ -164,23 +164,23 @@ __device__ RowMax scan_row(const DeltaPtrs& ch, int n, int i, bool exact_mode, i
         t1 = up ? v : t1;
         tj = up ? j : tj;
     }
-    group_top2<L>(t1, t2, tj);
+    const SymLead ld = group_sym_lead<L>(t1, t2, tj, r, gbase, rr);
     RowMax out;
-    if (!exact_mode && tj >= 0 &&
-        (t2 == -INFINITY || t1 - t2 > sym_err(t1, rr) + sym_err(t2, rr))) {
-        const ObjP q = ch.P[tj];
-        const float e = sym_val_exact(q.xf, q.yf, ch.RY[tj], rx, ry, (double)rr);
+    if (!exact_mode && ld.clear) {
+        const ObjP q = ch.P[ld.j];
+        const float e = sym_val_exact(q.xf, q.yf, ch.RY[ld.j], rx, ry, (double)rr);
         out.mx = fmaxf(0.0f, e);
-        out.arg = e > 0.0f ? tj : -1;
+        out.arg = e > 0.0f ? ld.j : -1;
         return out;
     }
-    const float thr = (exact_mode || tj < 0) ? INFINITY : 2.0f * sym_err(fabsf(t1) + 1.0f, rr);
+    const float thr =
+        (exact_mode || ld.j < 0) ? INFINITY : 2.0f * sym_err(fabsf(ld.m) + 1.0f, rr);
     float bv = -INFINITY;
     int bj = -1;
     for (int j = r; j < n; j += L) {
         const ObjP p = ch.P[j];
         const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
-        if (!(v < t1 - thr)) {
+        if (!(v < ld.m - thr)) {
             const float e = sym_val_exact(p.xf, p.yf, ch.RY[j], rx, ry, (double)rr);
             if (e > bv) {
                 bv = e;
@@ -256,7 +256,7 @@ __device__ void symmetry_delta(const DeltaPtrs& ch, int n, const RowBuf cur, con
         const int b = __builtin_ctzll(who);
         const int tb = __shfl(resc ? __builtin_ctzll(resc) : 0, gbase + b);
         const int i = tb * L + b;
-        const RowMax s = scan_row<L>(ch, n, i, exact_mode, r);
+        const RowMax s = scan_row<L>(ch, n, i, exact_mode, r, gbase);
         if (r == b) {
             nxt.put(i, s);
             resc &= resc - 1;
@@ -764,7 +764,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
     for (int ci = 0; ci < c; ++ci) nz_row<L>(ch, n, ci, r, gbase);
     rels_delta<L>(ch, nr, -2, -1, r);
     for (int i = 0; i < n; ++i) {
-        const RowMax s = scan_row<L>(ch, n, i, wild_cnt > 0, r);
+        const RowMax s = scan_row<L>(ch, n, i, wild_cnt > 0, r, gbase);
         if (r == (i % L)) ch.RB[0].put(i, s);
     }
     wave_sync();
