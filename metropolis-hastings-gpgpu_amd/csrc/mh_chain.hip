@@ -267,9 +267,19 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             const RectShape cs = ch.clrs[i];
             const ObjP ps = ch.P[cs.pad];
             ch.CLA[i] = shape_box(cs, ps.xf, ps.yf);             // ClearanceCosts, :414-415
-            const ObjP pi = ch.P[i];                              // SurfaceArea quirk: cfg[i], :456
-            sac[m] = comp_overlaps(rm, shape_box(cs, pi.xf, pi.yf));
         }
+        // SurfaceArea quirk: clearance i at object i's pose (cfg[i], :456). Steps with one
+        // object per lane keep the overlaps unless object i moved, so most steps skip the pass.
+        bool sa_new = i < c;
+        if constexpr (SHARED) {
+            sac[m] = clp.sac;
+            sa_new = sa_new && (i == ka || i == kb);
+        }
+        if (sa_new) {
+            const ObjP pi = ch.P[i];
+            sac[m] = comp_overlaps(rm, shape_box(ch.clrs[i], pi.xf, pi.yf));
+        }
+        if constexpr (NPL == 1) clo.sac = sac[0];
     }
     }
     wave_sync();

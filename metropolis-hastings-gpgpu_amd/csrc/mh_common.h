@@ -636,6 +636,7 @@ struct ClPairs {
     int buf;
     double rpw, rang;  // this lane's relationship terms (kept for relationships a move misses)
     float cph;         // this lane's object's cos(phi) (kept for objects a move misses)
+    float4 sac;        // SurfaceArea overlaps of clearance `lane` at object `lane`'s pose
 };
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
