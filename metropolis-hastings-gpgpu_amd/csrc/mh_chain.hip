@@ -391,14 +391,22 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         need[m] = row && (i == ka || i == kb);
         pend[m] = 0u;
         if (row && !need[m]) {
+            // A changed column's pair is pending (exact value needed) unless its estimate is
+            // certainly below the old maximum; if that column held the maximum, the maximum
+            // certainly dropped and the row is re-scanned without the exact value.
             if (ka >= 0) {
                 const float v = sym_val_fast(qa, rxs[m], rys[m], rrs[m]);
-                if (ca == ka || exact_mode || !(v + sym_err(v, rrs[m]) < cm)) pend[m] |= 1u;
+                const bool below = !exact_mode && v + sym_err(v, rrs[m]) < cm;
+                if (ca == ka && below) need[m] = true;
+                else if (!below) pend[m] |= 1u;
             }
             if (kb >= 0) {
                 const float v = sym_val_fast(qb, rxs[m], rys[m], rrs[m]);
-                if (ca == kb || exact_mode || !(v + sym_err(v, rrs[m]) < cm)) pend[m] |= 2u;
+                const bool below = !exact_mode && v + sym_err(v, rrs[m]) < cm;
+                if (ca == kb && below) need[m] = true;
+                else if (!below) pend[m] |= 2u;
             }
+            if (need[m]) pend[m] = 0u;
         }
         any_pend |= pend[m] != 0u;
     }

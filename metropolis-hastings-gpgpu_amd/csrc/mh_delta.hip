@@ -213,15 +213,23 @@ __device__ void symmetry_delta(const DeltaPtrs& ch, int n, const RowBuf cur, con
         }
         float rx, ry, rr;
         row_setup(ch, i, rx, ry, rr);
+        // pending unless certainly below the old maximum; a maximum held by the changed
+        // column that certainly dropped sends the row straight to the re-scan
         if (ka >= 0) {
             const float v = sym_val_fast(qa, rx, ry, rr);
-            if (c0.arg == ka || exact_mode || !(v + sym_err(v, rr) < c0.mx)) pa |= 1ull << t;
+            const bool below = !exact_mode && v + sym_err(v, rr) < c0.mx;
+            if (c0.arg == ka && below) resc |= 1ull << t;
+            else if (!below) pa |= 1ull << t;
         }
         if (kb >= 0) {
             const float v = sym_val_fast(qb, rx, ry, rr);
-            if (c0.arg == kb || exact_mode || !(v + sym_err(v, rr) < c0.mx)) pb |= 1ull << t;
+            const bool below = !exact_mode && v + sym_err(v, rr) < c0.mx;
+            if (c0.arg == kb && below) resc |= 1ull << t;
+            else if (!below) pb |= 1ull << t;
         }
     }
+    pa &= ~resc;
+    pb &= ~resc;
     // Exact values of the pending (row, column) pairs, one per lane per pass.
     while (__ballot((pa | pb) != 0)) {
         if (pa | pb) {
