@@ -760,8 +760,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         len = (len + 3) & ~3;
         // The Clearance list (float terms, float accumulator) usually outruns the dense sums:
         // its part past them runs in plain fp32 below (rn_f(a + b) is the reference's float add).
-        const int len_main = (k == 4) ? min(len, a.lay.N4) : len;
-        const int steps = group_max<L>(len_main);
+        // The walk's length comes from the group-uniform counts, with no cross-lane reduction.
+        const int steps = max(a.lay.N4, max((cnt_pw + 3) & ~3, (cnt_ang + 3) & ~3));
         double accd = acc0, accf = acc0;
         for (int l0 = 0; l0 < steps; l0 += 4) {
             // every stream holds doubles; a lane past its end reads four zeros
