@@ -178,6 +178,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     double px[NPL], py[NPL];
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
+    float4 boxo[NPL];  // each owned object's box at its pose (SurfaceArea, Clearance pairs)
     double rpw[NPL], rang[NPL];  // relationship terms of chunks m < NPL (see Phase F)
     bool wild = false;  // a pose outside the range the fp32 symmetry estimate is proven for
     for (int rep = 0; rep < MH_REPS(1); ++rep) {
@@ -187,7 +188,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         const int i = m * L + r;
         px[m] = py[m] = 0.0;
         cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
-        sao[m] = sac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sao[m] = sac[m] = boxo[m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n) {
             const RectShape os = ch.objs[i];
             const float area = __int_as_float(os.pad);
@@ -215,9 +216,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
             rrs[m] = rr;
             // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
-            float4 box = shape_box(os, p.xf, p.yf);
+            const float4 box = shape_box(os, p.xf, p.yf);
             if constexpr (WITH_OL) ch.OFF[i] = box;
             sao[m] = comp_overlaps(rm, box);
+            boxo[m] = box;
         }
         rpw[m] = rang[m] = 0.0;
         if constexpr (SHARED) {
@@ -588,8 +590,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     bool cl_done = false;
     if constexpr (NPL == 1) {
         const int j = r;
-        const float4 boxj = j < n ? shape_box(ch.objs[j], ch.P[j].xf, ch.P[j].yf)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 boxj = boxo[0];
         if constexpr (INC_CL) {
             const uint64_t* NZc = ch.NZ + clp.buf * c;
             uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
