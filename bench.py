@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark: MH chain-steps/s on the 64-object synthetic room (BASELINE.json config 3).
 
-One bench "step" = one launch of the chain kernel that advances every chain of this GPU's
-shard by --iters MH steps (propose -> Costs -> accept, Kernel.cu:785-828), state resident in
-HBM/LDS. value = (all ranks' chains) x (timed MH steps) / max-over-ranks wall time.
+One bench "step" advances every chain of this GPU's shard by --iters MH steps (propose ->
+Costs -> accept, Kernel.cu:785-828; 4,000 by default, i.e. four 1,000-step kernel launches),
+state resident in HBM/LDS. The driver's `--steps 20 --warmup 5` and the defaults (24 + 1) both
+run config 3's full 100,000 MH steps per chain, so mean_final_cost is the config's own.
+value = (all ranks' chains) x (timed MH steps) / max-over-ranks wall time.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
 per GPU, chains sharded by global id (chain c always draws Philox subsequence c), no collective
@@ -30,6 +32,7 @@ import __graft_entry__ as graft  # noqa: E402
 
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (== FP32 MFMA peak)
 HBM_PEAK_GBS = 8000.0
+STEPS_PER_LAUNCH = 1000  # the library's launch chunk (mh_abi.cpp kStepsPerLaunch)
 
 
 def algorithmic_flops(n: int, c: int, r: int) -> int:
@@ -72,9 +75,22 @@ def combine_records(recs):
             "accepted": int(sum(r[4] for r in recs))}
 
 
-def cpu_baseline(room, orc, seed: int, budget_s: float, threads: int):
+def host_cores():
+    """(threads the CPU baseline uses, nproc, CPUs this process may run on). The GPU box grants
+    a one-GPU job a 16-CPU share of a larger machine whose CPUs nproc counts in full, so the
+    baseline runs on min(affinity, 16) threads and reports all three numbers."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    return max(1, min(affinity, 16)), nproc, affinity
+
+
+def cpu_baseline(room, orc, seed: int, budget_s: float):
     """Oracle chain (the reference's algorithm, Kernel.cu:777-828, OffLimits included as the
-    reference computes it every step) on `threads` host cores, bounded to ~budget_s."""
+    reference computes it every step) on the host's cores, bounded to ~budget_s."""
+    threads, nproc, affinity = host_cores()
     t0 = time.perf_counter()
     orc.run_chains(room, threads, 20, seed, threads=threads)
     per = (time.perf_counter() - t0) / (threads * 20) * threads  # seconds per chain-step/thread
@@ -84,15 +100,16 @@ def cpu_baseline(room, orc, seed: int, budget_s: float, threads: int):
     orc.run_chains(room, chains, steps, seed, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": chains * steps / dt, "unit": "chain-steps/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "host_nproc": nproc, "host_affinity_cpus": affinity,
             "sample": f"oracle/mh_oracle.c chain on {room.name}: {chains} chains x {steps} steps"
-                      f" ({dt:.1f} s, {threads} threads)"}
+                      f" ({dt:.1f} s, {threads} threads; nproc {nproc}, {affinity} CPUs in this"
+                      f" process's affinity, 16 of them the box's per-GPU share)"}
 
 
-def pmc_record(n_chains_per_launch: int, step_kernel: str):
-    """The committed rocprofv3 PMC record of the step kernel (profiles/pmc_step_kernel.json,
+def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str):
+    """The committed rocprofv3 PMC record of the step kernel (profiles/pmc_step_kernel_n<N>.json,
     written by tools/pmc_summary.py --json) if it was taken on this workload, else {}."""
-    p = ROOT / "profiles" / "pmc_step_kernel.json"
+    p = ROOT / "profiles" / f"pmc_step_kernel_n{n}.json"
     if not p.exists():
         return {}
     try:
@@ -105,20 +122,24 @@ def pmc_record(n_chains_per_launch: int, step_kernel: str):
         return {}
 
 
+CONFIG_NAMES = {(64, 65536): "config 3: ", (256, 32768): "config 5: ", (8, 1024): "config 2: "}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=99,
-                    help="timed launches (1 warmup + 99 = the config's 100k MH steps)")
+    ap.add_argument("--steps", type=int, default=24,
+                    help="timed bench steps (1 warmup + 24 = the config's 100k MH steps)")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--iters", type=int, default=1000, help="MH steps per launch (<= 1000)")
+    ap.add_argument("--iters", type=int, default=4000, help="MH steps per bench step")
     ap.add_argument("--objects", type=int, default=64)
     ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    args.iters = max(1, min(args.iters, 1000))
+    args.iters = max(1, args.iters)
+    launches_per_step = -(-args.iters // STEPS_PER_LAUNCH)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -197,9 +218,11 @@ def main() -> int:
     chain_steps = total_chains * args.steps * args.iters
     value = chain_steps / wall
     ms_per_step = wall * 1e3 / args.steps
-    launch_s = kernel_ms / 1e3 / args.steps  # average duration of one step-kernel launch
+    launches = args.steps * launches_per_step
+    launch_s = kernel_ms / 1e3 / launches  # average duration of one step-kernel launch
+    iters_per_launch = args.iters / launches_per_step
     f = algorithmic_flops(n, c, r)
-    achieved = args.chains * args.iters * f / launch_s / 1e12
+    achieved = args.chains * iters_per_launch * f / launch_s / 1e12
     bytes_launch = args.chains * state_bytes_per_chain(n)
 
     out = None
@@ -207,11 +230,10 @@ def main() -> int:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             orc = graft.load_oracle()
-            threads = max(1, min(16, os.cpu_count() or 1))
-            cpu = cpu_baseline(room, orc, args.seed, args.cpu_budget, threads)
-        pmc = pmc_record(args.chains, step_kernel)
+            cpu = cpu_baseline(room, orc, args.seed, args.cpu_budget)
+        pmc = pmc_record(n, args.chains, step_kernel)
         out = {
-            "metric": "MH chain-steps/sec (whole node) + mean final cost, N=64 objects",
+            "metric": f"MH chain-steps/sec (whole node) + mean final cost, N={n} objects",
             "value": value,
             "unit": "chain-steps/s",
             "n_gpus": world,
@@ -224,9 +246,9 @@ def main() -> int:
             "dtype": "f64+f32 (reference precision map)",
             "data": "synthetic (SURVEY.md 8(d) room, splitmix64 seed 0x5EED0000+N)",
             "config": {
-                "workload": ("config 3: " if (n, args.chains) == (64, 65536) else "")
+                "workload": CONFIG_NAMES.get((n, args.chains), "")
                             + f"{n}-object synthetic room, {args.chains} chains per GPU,"
-                            f" {args.iters} MH steps per launch",
+                            f" {args.iters} MH steps per bench step",
                 "objects": n, "clearances": c, "relationships": r,
                 "chains_per_gpu": args.chains, "global_chains": total_chains,
                 "mh_steps_per_step": args.iters,
@@ -238,8 +260,10 @@ def main() -> int:
             "mean_final_cost": mean_cost,
             "best_final_cost": best_cost,
             "best_chain": best_chain,
+            "accepted": job["accepted"],
             "accept_rate": accept_rate,
             "kernel_ms_per_step": kernel_ms / args.steps,
+            "kernel_ms_per_launch": launch_s * 1e3,
             "roofline": {
                 "bound": "valu",
                 "achieved": achieved,
@@ -255,6 +279,10 @@ def main() -> int:
                 "executed_valu_wave_insts_per_chain_step": (
                     pmc["valu_wave_insts_per_launch"] / (args.chains * pmc["iters_per_launch"])
                     if pmc.get("valu_wave_insts_per_launch") else None),
+                # VALU issue utilisation of the profiled launch (tools/pmc_summary.py): busy
+                # SIMD cycles priced per instruction class / (1024 SIMDs x kernel cycles)
+                "valu_issue_util": pmc.get("valu_issue_util"),
+                "pmc_source": pmc.get("source"),
             },
             "cpu_baseline": cpu,
         }

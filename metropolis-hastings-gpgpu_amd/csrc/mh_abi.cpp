@@ -340,6 +340,8 @@ uint64_t seed_from_env() {
 struct mh_session {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t last = nullptr;    // the stream the session's latest work was queued on
+    hipEvent_t done = nullptr;     // recorded on `last` after that work
     Room room;
     Geometry geo{};
     int64_t n_chains = 0, chain_offset = 0;
@@ -399,6 +401,7 @@ void free_session(mh_session* s) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->done) (void)hipEventSynchronize(s->done);  // work queued on a caller's stream
     (void)hipFree(s->d_obj);
     (void)hipFree(s->d_clr);
     (void)hipFree(s->d_rel);
@@ -412,6 +415,7 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_pts);
     (void)hipFree(s->d_costs);
     (void)hipFree(s->d_summary);
+    if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     (void)hipSetDevice(prev);
     delete s;
@@ -424,9 +428,26 @@ bool upload(T** dst, const std::vector<T>& src, hipStream_t st) {
     return true;
 }
 
+// Orders work about to be queued on `st` after everything the session queued before, on
+// whichever stream that was (its own stream for the setup, a caller's stream for a run; the
+// event was recorded there, so that stream may since have been destroyed).
+bool order_after_last(mh_session* s, hipStream_t st) {
+    if (st != s->last) MH_TRY_HIP(hipStreamWaitEvent(st, s->done, 0));
+    return true;
+}
+
+// Marks the end of the work just queued on `st`.
+bool record_done(mh_session* s, hipStream_t st) {
+    MH_TRY_HIP(hipEventRecord(s->done, st));
+    s->last = st;
+    return true;
+}
+
 bool session_init(mh_session* s) {
     MH_TRY_HIP(hipSetDevice(s->device));
     MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    MH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    s->last = s->stream;
     if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->geo)) return false;
     if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
@@ -455,7 +476,7 @@ bool session_init(mh_session* s) {
     MH_TRY_HIP(hipMalloc((void**)&s->d_costs, sizeof(resultCosts) * nc));
     MH_TRY_HIP(hipMalloc((void**)&s->d_summary, sizeof(mh_summary)));
     MH_TRY_HIP(mh::launch(mh::OP_INIT, s->args(), s->geo.L, s->geo.npl, s->geo.waves, s->stream));
-    return true;
+    return record_done(s, s->stream);
 }
 
 hipStream_t pick_stream(const mh_session* s, void* stream) {
@@ -464,14 +485,7 @@ hipStream_t pick_stream(const mh_session* s, void* stream) {
 
 bool session_run(mh_session* s, int iterations, hipStream_t st) {
     MH_TRY_HIP(hipSetDevice(s->device));
-    if (st != s->stream) {
-        // Order the session's own setup work before work on a caller stream.
-        hipEvent_t ev;
-        MH_TRY_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        MH_TRY_HIP(hipEventRecord(ev, s->stream));
-        MH_TRY_HIP(hipStreamWaitEvent(st, ev, 0));
-        MH_TRY_HIP(hipEventDestroy(ev));
-    }
+    if (!order_after_last(s, st)) return false;
     mh::LaunchArgs a = s->args();
     for (int done = 0; done < iterations;) {
         int chunk = std::min(kStepsPerLaunch, iterations - done);
@@ -485,16 +499,17 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
         if (s->n_temps > 1 && s->steps_done % s->swap_interval == 0)
             MH_TRY_HIP(mh::launch_exchange(a, s->d_perm, (int)(s->steps_done / s->swap_interval), st));
     }
-    return true;
+    return record_done(s, st);
 }
 
 bool session_finalize(mh_session* s, hipStream_t st) {
     MH_TRY_HIP(hipSetDevice(s->device));
+    if (!order_after_last(s, st)) return false;
     mh::LaunchArgs a = s->args();
     a.lay = s->geo.lay_ol;
     if (s->track != mh::TRACK_OFF) a.st = s->d_best;  // report each chain's best configuration
     MH_TRY_HIP(mh::launch(mh::OP_FINAL, a, s->geo.L, s->geo.npl, s->geo.waves_ol, st));
-    return true;
+    return record_done(s, st);
 }
 
 bool session_download(mh_session* s, point* pts, resultCosts* costs) {

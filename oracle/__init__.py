@@ -78,6 +78,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_rand_int.restype = C.c_int
     lib.orc_pick_object.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     lib.orc_pick_object.restype = C.c_int
+    lib.orc_index_n_draws.argtypes = [C.c_int]
+    lib.orc_index_n_draws.restype = C.c_longlong
     lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.orc_accept.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.orc_accept.restype = C.c_int
@@ -169,6 +171,11 @@ def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int =
             d[:, :, k] = raw[:, :, 8 * k:8 * k + 8].copy().view(np.float64)[:, :, 0]
         return d, c8, a
     return np.frombuffer(bytes(buf), dtype=np.float32).reshape(chains, n, 6).copy(), c8, a
+
+
+def index_n_draws(reset: bool = False) -> int:
+    """Draws of index nObjs (u == 1.0f, Kernel.cu:566-574) the oracle's picks have seen."""
+    return int(load().orc_index_n_draws(1 if reset else 0))
 
 
 def rng_init(seed: int, subsequence: int, kind: int = PHILOX) -> OrcRng:

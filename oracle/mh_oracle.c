@@ -540,10 +540,24 @@ static int rand_int(orc_rng* r, int max, int min) {
 
 int orc_rand_int(orc_rng* r, int max, int min) { return rand_int(r, max, min); }
 
+/* Draws of index nObjs seen by pick_object in this process (test diagnostic: lets a test
+ * prove that a fixture exercises the u == 1.0f edge of Kernel.cu:566-574). */
+static long long g_index_n_draws;
+
+long long orc_index_n_draws(int reset) {
+    const long long v = __atomic_load_n(&g_index_n_draws, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_index_n_draws, 0, __ATOMIC_RELAXED);
+    return v;
+}
+
 /* Object pick with redraw while frozen (Kernel.cu:598-602); index nObjs is frozen. */
 static int pick_object(const positionAndRotation* cfg, int n, orc_rng* r) {
     int k = rand_int(r, n - 1, 0);
-    while (k >= n || cfg[k].frozen) k = rand_int(r, n - 1, 0);
+    for (;;) {
+        if (k >= n) __atomic_add_fetch(&g_index_n_draws, 1, __ATOMIC_RELAXED);
+        else if (!cfg[k].frozen) break;
+        k = rand_int(r, n - 1, 0);
+    }
     return k;
 }
 

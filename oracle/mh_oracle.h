@@ -88,6 +88,8 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
  * (Kernel.cu:598-602; index nObjs counts as frozen). */
 int orc_rand_int(orc_rng* r, int max, int min);
 int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r);
+/* How many times pick_object drew index nObjs (u == 1.0f) in this process; reset if asked. */
+long long orc_index_n_draws(int reset);
 
 /* One proposal (Kernel.cu:576-704) applied in place to cfg (nObjs entries). */
 void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r);

@@ -10,6 +10,7 @@
 * rooms: hashes of the synthetic rooms' wire bytes (SURVEY.md 8(d) generator).
 * xorwow_rocrand: the first draws of rocRAND's own XORWOW engine (xorwow_rocrand.cpp, built here
   with hipcc for the host) -- pins the oracle's XORWOW recurrence and subsequence jump.
+* index_n: chains whose pick draws u == 1.0f early (written by find_index_n.py; kept here).
 * xorwow_curand / chains_xorwow: the oracle's cuRAND-XORWOW streams and seeded chain runs in
   that mode (the HIP path must reproduce them bit for bit).
 
@@ -110,6 +111,8 @@ def main():
     out["rooms"] = {f"synthetic{n}": hashlib.sha256(room_bytes(mh.synthetic_room(n))).hexdigest()
                     for n in (1, 8, 64, 256)}
     path = Path(__file__).with_name("golden.json")
+    if path.exists():  # searched fixtures (find_index_n.py) are kept
+        out["index_n"] = json.loads(path.read_text()).get("index_n", [])
     path.write_text(json.dumps(out, indent=1) + "\n")
     print("wrote", path)
 

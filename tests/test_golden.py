@@ -79,3 +79,17 @@ def test_golden_chains_xorwow_oracle(mh, orc, case):
     assert make_golden.sha(st.astype(np.float32)) == case["points_sha256"]
     assert make_golden.sha(costs) == case["costs_sha256"]
     assert int(acc.sum()) == case["accepted"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["index_n"], ids=lambda c: f"chain{c['chain']}")
+def test_index_n_fixture_reaches_the_edge(mh, orc, case):
+    """The searched chains (find_index_n.py) draw index nObjs (u == 1.0f, Kernel.cu:566-574)
+    at step `first_step` and not before; the defined semantics redraw it."""
+    room = mh.synthetic_room(case["n"])
+    orc.index_n_draws(reset=True)
+    orc.run_chains(room, 1, case["first_step"] - 1, case["seed"], chain_begin=case["chain"])
+    assert orc.index_n_draws() == 0
+    orc.index_n_draws(reset=True)
+    _, costs, _ = orc.run_chains(room, 1, case["steps"], case["seed"], chain_begin=case["chain"])
+    assert orc.index_n_draws() >= 1
+    assert np.isfinite(costs).all()

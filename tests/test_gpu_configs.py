@@ -1,0 +1,270 @@
+"""BASELINE.json's configurations at their real lengths, the per-GPU path of the 8-GPU config, and
+the reference edges that short runs do not reach -- each chain bit for bit against the oracle
+(oracle/mh_oracle.c, the restatement of KernelFolder/Kernel/Kernel.cu:754-828).
+
+* config 2: the 8-object room, all 1,024 chains x 10k steps;
+* config 3: 64 chains sampled by global id out of a 65,536-chain, 100k-step session;
+* config 4: one rank's shard (global ids 7*65,536 ...), the 2-rank bench.py launcher path, and
+  KernelWrapper's in-process $MH_DEVICES sharding (unmeasured on 8 GPUs: the driver runs those);
+* config 5: 8 chains sampled out of a 32,768-chain, 10k-step session of the 256-object room;
+* the index-n pick (u == 1.0f, Kernel.cu:566-574,598-602) on every RNG path, from a searched
+  fixture (tests/golden/find_index_n.py);
+* KernelWrapper's $MH_SEED against KernelWrapperSeeded (Kernel.cu:873,943);
+* the incremental kernel's list-overflow windows (a room where every Clearance pair overlaps).
+
+Every check asserts zero forked chains and reports the count as a ParityReport warning, which
+`pytest -q` keeps in its summary.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from parity_util import check_chains
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = json.loads((ROOT / "tests" / "golden" / "golden.json").read_text())
+HOST_THREADS = 16  # the GPU box's CPU share per GPU
+
+
+def _oracle_blocks(orc, room, starts, per, steps, seed, threads_each):
+    """Oracle chains [b, b + per) for every b in starts, the blocks run concurrently (ctypes
+    releases the GIL); returns (points, costs, global ids) in block order."""
+    def one(b):
+        return orc.run_chains(room, per, steps, seed, chain_begin=b, threads=threads_each)
+    with ThreadPoolExecutor(len(starts)) as ex:
+        res = list(ex.map(one, starts))
+    ids = np.concatenate([np.arange(b, b + per) for b in starts])
+    return (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]), ids)
+
+
+def _session_sampled(mh, orc, room, chains, steps, seed, starts, per, threads_each, offset=0):
+    """Runs a full-size session (launches queued asynchronously) while the oracle runs the
+    sampled blocks, then returns both."""
+    with mh.Session(room, chains, seed=seed, chain_offset=offset) as s:
+        s.run(steps)
+        ref_pts, ref_costs, ids = _oracle_blocks(orc, room, [offset + b for b in starts], per,
+                                                 steps, seed, threads_each)
+        s.finalize()
+        pts, costs = s.download()
+        summ = s.summary()
+    local = ids - offset
+    return pts, costs, summ, pts[local], costs[local], ref_pts, ref_costs, ids
+
+
+def _in_room(room, pts):
+    w = np.float32(room.surface_rectangle[0].x)
+    return bool(np.all((pts[..., 0] >= 0) & (pts[..., 0] <= w) & (pts[..., 1] >= 0) &
+                       (pts[..., 1] <= w)))
+
+
+def test_config2_full_length(mh, orc, hiplib):
+    """Config 2 in full: 8-object room, 1,024 chains x 10,000 steps, every chain."""
+    room = mh.synthetic_room(8)
+    chains, steps, seed = 1024, 10_000, 42
+    pts, costs = mh.kernel_wrapper(room, chains, steps, seed=seed)
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS)
+    check_chains("config 2 (N=8, 1024 x 10k)", pts, costs, ref_pts, ref_costs, report=True)
+
+
+def test_config3_full_length_sampled(mh, orc, hiplib):
+    """Config 3: a 65,536-chain session run for the config's 100,000 steps; 64 chains sampled
+    across the id range (8 blocks of 8) against the oracle by global id."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed = 65536, 100_000, 42
+    starts = [0, 9360, 18720, 28080, 37440, 46800, 56160, 65528]
+    pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
+        mh, orc, room, chains, steps, seed, starts, 8, 2)
+    check_chains("config 3 (N=64, 65536 x 100k, 64 sampled)", sp, sc, rp, rc, ids=ids,
+                 report=True)
+    assert summ.n_chains == chains and summ.best_total == costs[:, 0].max()
+    assert _in_room(room, pts)
+
+
+def test_config5_full_length_sampled(mh, orc, hiplib):
+    """Config 5: the 256-object room, a 32,768-chain session for 10,000 steps (incremental
+    kernel, 5 chains per CU); 8 chains sampled by global id against the oracle."""
+    room = mh.synthetic_room(256)
+    chains, steps, seed = 32768, 10_000, 42
+    starts = [0, 4681, 9362, 14043, 18724, 23405, 28086, 32767]
+    pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
+        mh, orc, room, chains, steps, seed, starts, 1, 1)
+    check_chains("config 5 (N=256, 32768 x 10k, 8 sampled)", sp, sc, rp, rc, ids=ids,
+                 report=True)
+    assert summ.n_chains == chains and _in_room(room, pts)
+
+
+def test_config4_rank7_shard(mh, orc, hiplib):
+    """Config 4's per-GPU work on one GPU: rank 7's shard (global ids [7*65536, 8*65536)),
+    64 chains sampled against the oracle at the same global ids (unmeasured on 8 GPUs)."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed, offset = 65536, 5_000, 42, 7 * 65536
+    starts = [0, 9360, 18720, 28080, 37440, 46800, 56160, 65528]
+    pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
+        mh, orc, room, chains, steps, seed, starts, 8, 2, offset=offset)
+    check_chains("config 4 rank-7 shard (N=64, 65536 x 5k, 64 sampled)", sp, sc, rp, rc,
+                 ids=ids, report=True)
+    assert summ.n_chains == chains
+    assert offset <= summ.best_chain < offset + chains
+    assert summ.best_total == costs[summ.best_chain - offset, 0]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_config4_two_rank_bench_equals_one_session(mh, hiplib, tmp_path):
+    """bench.py's multi-rank path as the driver launches it (torch.distributed.run, 2 ranks;
+    gloo because this box has one GPU): rank -> Session(chain_offset) -> summary -> all-gather
+    -> combine_records. The combined record must equal one Session over both shards."""
+    n, per, iters, steps, warmup, seed = 16, 2048, 100, 2, 1, 42
+    env = dict(os.environ, MH_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(ROOT / "bench.py"), "--gpus", "2", "--objects", str(n), "--chains", str(per),
+           "--iters", str(iters), "--steps", str(steps), "--warmup", str(warmup),
+           "--seed", str(seed), "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=env, cwd=tmp_path, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    room = mh.synthetic_room(n)
+    with mh.Session(room, 2 * per, seed=seed) as s:
+        s.run((steps + warmup) * iters)
+        s.finalize()
+        _, costs = s.download()
+        summ = s.summary()
+    assert rec["n_gpus"] == 2 and rec["config"]["global_chains"] == 2 * per
+    assert rec["best_chain"] == summ.best_chain
+    assert rec["best_final_cost"] == float(summ.best_total)
+    assert rec["accepted"] == summ.accepted
+    assert rec["mean_final_cost"] == pytest.approx(summ.sum_total / (2 * per), rel=1e-12)
+
+
+def test_kernelwrapper_mh_devices_sharding(mh, hiplib, monkeypatch):
+    """$MH_DEVICES=0,0: KernelWrapperSeeded shards the call over two host threads and streams
+    (device 0 twice); the result must equal the single-device call bit for bit."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed = 1000, 300, 4711
+    monkeypatch.delenv("MH_DEVICES", raising=False)
+    p1, c1 = mh.kernel_wrapper(room, chains, steps, seed=seed)
+    monkeypatch.setenv("MH_DEVICES", "0,0")
+    p2, c2 = mh.kernel_wrapper(room, chains, steps, seed=seed)
+    assert np.array_equal(p1.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))
+    monkeypatch.setenv("MH_DEVICES", "0,0,0")  # uneven shards, tracking and tempering groups
+    p3, c3 = mh.kernel_wrapper(room, 996, steps, seed=seed, track=2, temps=4, swap_interval=50,
+                               beta_min=0.5)
+    monkeypatch.delenv("MH_DEVICES")
+    p4, c4 = mh.kernel_wrapper(room, 996, steps, seed=seed, track=2, temps=4, swap_interval=50,
+                               beta_min=0.5)
+    assert np.array_equal(p3.view(np.uint32), p4.view(np.uint32))
+    assert np.array_equal(c3.view(np.uint32), c4.view(np.uint32))
+
+
+def test_kernelwrapper_mh_seed(mh, hiplib, monkeypatch):
+    """The reference's own symbol seeds from $MH_SEED (time(NULL) otherwise, Kernel.cu:943):
+    KernelWrapper with MH_SEED=s equals KernelWrapperSeeded(s)."""
+    room = mh.main_fixture()
+    monkeypatch.setenv("MH_SEED", "123456789")
+    p1, c1 = mh.kernel_wrapper(room, 256, 200)  # seed=None -> KernelWrapper
+    p2, c2 = mh.kernel_wrapper(room, 256, 200, seed=123456789)
+    assert np.array_equal(p1.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))
+
+
+STEP_PATHS = [  # (name, env): every RNG path a 64-object chain can take
+    ("full L=64 WaveRng", {"MH_DELTA": "0"}),
+    ("full L=32 ChainRng", {"MH_DELTA": "0", "MH_LANES": "32"}),
+    ("incremental", {"MH_DELTA": "1"}),
+    ("incremental L=64 WaveRng", {"MH_DELTA": "1", "MH_DELTA_LANES": "64"}),
+]
+
+
+@pytest.mark.parametrize("path", STEP_PATHS, ids=[p[0] for p in STEP_PATHS])
+@pytest.mark.parametrize("case", GOLDEN["index_n"], ids=lambda c: f"chain{c['chain']}")
+def test_index_n_pick_redrawn(mh, orc, hiplib, monkeypatch, case, path):
+    """A chain whose pick draws u == 1.0f: generateRandomIntInRange(63, 0) gives 64 = nObjs
+    (Kernel.cu:566-574), redrawn like a frozen object. The oracle must see the event; the device
+    must reproduce the chain bit for bit on every step kernel and RNG path."""
+    for k, v in path[1].items():
+        monkeypatch.setenv(k, v)
+    room = mh.synthetic_room(case["n"])
+    cid, steps, seed = case["chain"], case["steps"], case["seed"]
+    orc.index_n_draws(reset=True)
+    rp, rc, _ = orc.run_chains(room, 1, steps, seed, chain_begin=cid)
+    assert orc.index_n_draws() >= 1
+    with mh.Session(room, 1, seed=seed, chain_offset=cid) as s:
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    check_chains(f"index-n chain {cid} ({path[0]})", pts, costs, rp, rc, ids=[cid])
+
+
+def _crowded_room(mh, n):
+    """Every clearance box overlaps every object box at every reachable pose: a 0.5 m room
+    (translations clamp to it, Kernel.cu:613-630) and boxes of 0.5-2 m."""
+    room = mh.synthetic_room(n)
+    w = 0.5
+    for k, (x, y) in enumerate([(w, w), (w, 0.0), (0.0, 0.0), (0.0, w)]):
+        room.surface_rectangle[k].x, room.surface_rectangle[k].y = x, y
+    rng = np.random.default_rng(n)
+    for i in range(n):
+        room.cfg[i].x, room.cfg[i].y = rng.uniform(0, w, size=2)
+    room.srf.centroidX = room.srf.centroidY = w
+    room.srf.focalX, room.srf.focalY = w / 2, w
+    return room
+
+
+@pytest.mark.parametrize("lanes", ["64", "32"])
+def test_incremental_list_overflow_windows(mh, orc, hiplib, monkeypatch, lanes):
+    """The incremental kernel sums Clearance / SurfaceArea lists longer than its LDS capacity
+    (4*NP and NP terms, mh_device.h make_delta_layout) in windows rebuilt in place. Here all
+    C*N Clearance pairs are non-zero at every step (C*N = 6,400 >> 4*NP = 768), so every
+    step takes that path; bit for bit against the oracle."""
+    monkeypatch.setenv("MH_DELTA", "1")
+    monkeypatch.setenv("MH_DELTA_LANES", lanes)
+    n = 160
+    room = _crowded_room(mh, n)
+    c = room.srf.nClearances
+    np_pad = (n + 63) // 64 * 64
+    assert c * n > 4 * np_pad  # the list cannot fit: windows on every step
+    chains, steps, seed = 16, 120, 160
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel()[2] == "incremental" and s.step_kernel()[0] == int(lanes)
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    rp, rc, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS)
+    # the final states still have (nearly) every pair non-zero, far past the capacity
+    assert min(_nonzero_clearance_pairs(room, rp[k]) for k in range(chains)) > 4 * np_pad
+    check_chains(f"crowded N={n} incremental L={lanes}", pts, costs, rp, rc)
+
+
+def _nonzero_clearance_pairs(room, pts):
+    """Non-zero ClearanceCosts pairs (Kernel.cu:408-431) of one configuration (float points),
+    with minValue's untranslated first x (:371)."""
+    v = np.array([(q.x, q.y) for q in room.vertices])
+
+    def box(p1, tx, ty):
+        q = v[p1:p1 + 4]
+        return (min(q[0, 0], *(q[1:, 0] + tx)), (q[:, 1] + ty).min(), (q[:, 0] + tx).max(),
+                (q[:, 1] + ty).max())
+    objs = [box(room.offlimits[j].point1Index, pts[j, 0], pts[j, 1]) for j in range(room.n)]
+    cnt = 0
+    for i in range(room.srf.nClearances):
+        s = room.clearances[i].SourceIndex
+        a = box(room.clearances[i].point1Index, pts[s, 0], pts[s, 1])
+        for b in objs:
+            cnt += max(a[0], b[0]) < min(a[2], b[2]) and max(a[1], b[1]) < min(a[3], b[3])
+    return cnt

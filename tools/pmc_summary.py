@@ -50,8 +50,22 @@ def main():
     d = {}
     if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_VALU" in c:
         d["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
-    if "SQ_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
-        d["sq_busy_frac"] = c["SQ_BUSY_CYCLES"] / c["GRBM_GUI_ACTIVE"]
+    if "GRBM_GUI_ACTIVE" in c:
+        simd_cycles = 1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0
+        d["kernel_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / 8.0
+        if "SQ_INSTS_VALU" in c:
+            d["valu_issue_util_flat"] = 2.0 * c["SQ_INSTS_VALU"] / simd_cycles
+            extra = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                     "SQ_INSTS_VALU_CVT", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_TRANS_F64")
+            if all(k in c for k in extra):
+                busy = 2.0 * c["SQ_INSTS_VALU"] + 2.0 * (
+                    c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] +
+                    c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_CVT"] +
+                    c["SQ_INSTS_VALU_TRANS_F32"]) + 6.0 * c["SQ_INSTS_VALU_TRANS_F64"]
+                d["valu_busy_simd_cycles"] = busy
+                d["valu_issue_util"] = busy / simd_cycles
+    if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        d["wait_inst_any_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
     if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
         d["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
     if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
@@ -70,6 +84,9 @@ def main():
                "iters_per_launch": a.iters,
                "valu_wave_insts_per_launch": c.get("SQ_INSTS_VALU"),
                "salu_insts_per_launch": c.get("SQ_INSTS_SALU"),
+               "valu_issue_util": d.get("valu_issue_util"),
+               "valu_issue_util_flat": d.get("valu_issue_util_flat"),
+               "valu_pricing": "2 cyc/VALU; +2 fp64 add/mul/fma, cvt, f32 trans; +6 f64 trans",
                "source": os.path.normpath(a.tag_dir)}
         with open(a.json, "w") as fh:
             json.dump(rec, fh, indent=1)
