@@ -259,8 +259,12 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     if (g.dL == 0 || best_chains <= 0) g.delta = false;  // does not fit: full evaluation
 }
 
-bool choose_geometry(int n, int c, int r, int device, Geometry& g) {
-    g.L = mh::choose_lanes(n);
+bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, Geometry& g) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1)
+        cus = 256;
+    // waves the full-evaluation step keeps resident: four per SIMD (LDS-bound at N = 64)
+    g.L = mh::choose_lanes(n, n_chains, 16LL * cus);
     g.npl = mh::choose_npl(n, g.L);
     if (g.npl > mh::max_npl()) {
         set_error("nObjs too large (max " + std::to_string(64 * mh::max_npl()) + ")");
@@ -448,7 +452,8 @@ bool session_init(mh_session* s) {
     MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     MH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
     s->last = s->stream;
-    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->geo)) return false;
+    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->n_chains, s->geo))
+        return false;
     if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
     if (!upload(&s->d_rel, s->room.rel, s->stream)) return false;

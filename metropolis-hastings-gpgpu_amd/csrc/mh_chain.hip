@@ -1412,15 +1412,20 @@ static hipError_t launch_geom(int op, const LaunchArgs& a, int waves_per_wg, hip
 namespace mh {
 
 // Lanes per chain: the next power of two >= N (at least 8, at most 64); objects per lane
-// (NPL) covers N > 64.
-int choose_lanes(int n) {
+// (NPL) covers N > 64. When the chains are too few to fill the GPU at that width, chains get
+// wider, up to a wavefront each, while their waves still fit `resident_waves` (a step's
+// critical path is shorter with one chain per wavefront: readlane instead of ds_bpermute, the
+// wave-batched RNG, the incremental clearance and atan2 passes; config 2, N = 8 x 1,024 chains:
+// 9.0e7 chain-steps/s at L = 8, 1.24e8 at 32, 1.73e8 at 64). $MH_LANES pins the width.
+int choose_lanes(int n, int64_t n_chains, int64_t resident_waves) {
     int L = 8;
     while (L < n && L < 64) L <<= 1;
     if (const char* e = getenv("MH_LANES")) {  // tuning override: 8, 16, 32 or 64
         const int want = atoi(e);
         if ((want == 8 || want == 16 || want == 32 || want == 64) && (n + want - 1) / want <= 8)
-            L = want;
+            return want;
     }
+    while (L < 64 && n_chains * (2 * L) <= resident_waves * 64) L <<= 1;
     return L;
 }
 int choose_npl(int n, int L) { return (n + L - 1) / L; }

@@ -40,7 +40,7 @@ struct LaunchArgs {
     DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
 };
 
-int choose_lanes(int n);
+int choose_lanes(int n, int64_t n_chains, int64_t resident_waves);
 int choose_npl(int n, int L);
 int max_npl();
 size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg);

@@ -33,6 +33,31 @@ def _room(mh, kind: str, n: int):
     return room
 
 
+def _narrow_lanes(n: int) -> int:
+    """The narrowest full-evaluation width for N objects (next power of two >= N, 8..64): the
+    library widens chains when they are few (choose_lanes), so the tests pin the narrow
+    instances (several chains per wavefront) explicitly."""
+    L = 8
+    while L < n and L < 64:
+        L *= 2
+    return L
+
+
+STEPS = ["incremental", "full", "full-narrow"]
+
+
+def _use_step(monkeypatch, step: str, n: int) -> str:
+    """Selects the step kernel (MH_DELTA) and, for "full-narrow", the narrow width (MH_LANES);
+    returns the step-kernel kind the session must report."""
+    kind = step.split("-")[0]
+    monkeypatch.setenv("MH_DELTA", "1" if kind == "incremental" else "0")
+    if step == "full-narrow":
+        if _narrow_lanes(n) == 64:
+            pytest.skip("the narrow instance is the default one for this N")
+        monkeypatch.setenv("MH_LANES", str(_narrow_lanes(n)))
+    return kind
+
+
 def _random_cfgs(mh, room, k: int, seed: int):
     """k configurations of room.n objects: uniform poses plus out-of-room objects, rotY at 0,
     2*PI and just inside, swapped duplicates, and coincident objects."""
@@ -123,7 +148,12 @@ def test_costs_match_oracle(mh, orc, hiplib, kind, n):
     ("syn", 100, 16, 60),        # NPL = 2
     ("syn", 256, 8, 25),         # config 5's room
 ])
-def test_chains_match_oracle(mh, orc, hiplib, kind, n, chains, steps):
+@pytest.mark.parametrize("geometry", ["default", "narrow"])
+def test_chains_match_oracle(mh, orc, hiplib, monkeypatch, geometry, kind, n, chains, steps):
+    if geometry == "narrow":
+        if _narrow_lanes(n) == 64:
+            pytest.skip("the narrow instance is the default one for this N")
+        monkeypatch.setenv("MH_LANES", str(_narrow_lanes(n)))
     room = _room(mh, kind, n)
     seed = 1000 + n
     pts, costs = mh.kernel_wrapper(room, chains, steps, seed=seed)
@@ -131,7 +161,7 @@ def test_chains_match_oracle(mh, orc, hiplib, kind, n, chains, steps):
     check_chains(f"{kind} N={n} {chains}x{steps}", pts, costs, ref_pts, ref_costs)
 
 
-@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("step", STEPS)
 @pytest.mark.parametrize("kind,n,chains,steps", [
     ("main", 32, 128, 300),
     ("frozen", 16, 128, 400),
@@ -147,11 +177,11 @@ def test_chains_match_oracle_each_step_kernel(mh, orc, hiplib, monkeypatch, step
                                               chains, steps):
     """Both step kernels (MH_DELTA=1: incremental evaluation, mh_delta.hip; MH_DELTA=0: full
     evaluation, mh_chain.hip) against the oracle, whichever is the default for N."""
-    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    kind_ = _use_step(monkeypatch, step, n)
     room = _room(mh, kind, n)
     seed = 7000 + n
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -312,7 +342,7 @@ def test_group_collectives(mh, hiplib, L):
             assert np.all(got["imax"][sl] == ig.max()) and np.all(got["isum"][sl] == ig.sum())
 
 
-@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("step", STEPS)
 @pytest.mark.parametrize("track", [1, 2])
 @pytest.mark.parametrize("kind,n,chains,steps", [
     ("main", 32, 96, 300),
@@ -326,11 +356,11 @@ def test_best_of_chain_matches_oracle(mh, orc, hiplib, monkeypatch, step, track,
     """Best-of-chain tracking (KernelWrapperEx / mh_session_create_ex; the reference's
     commented-out cfgBest, Kernel.cu:779-782,808-816,840-860) against the oracle's restatement:
     the best configuration and its eight costs, bit for bit, for both step kernels."""
-    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    kind_ = _use_step(monkeypatch, step, n)
     room = _room(mh, kind, n)
     seed = 9100 + n + track
     with mh.Session(room, chains, seed=seed, track=track) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -420,7 +450,7 @@ def test_golden_chains_xorwow_hip(mh, hiplib, case):
     assert MAKE_GOLDEN.sha(costs) == case["costs_sha256"]
 
 
-@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("step", STEPS)
 @pytest.mark.parametrize("kind,n,chains,steps", [
     ("main", 32, 128, 300),
     ("frozen", 16, 128, 400),
@@ -431,11 +461,11 @@ def test_golden_chains_xorwow_hip(mh, hiplib, case):
 def test_xorwow_chains_match_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, chains, steps):
     """Chains seeded exactly as the reference seeds them (curand_init(seed + c, c, 0),
     Kernel.cu:159,943) against the oracle, bit for bit, for both step kernels."""
-    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    kind_ = _use_step(monkeypatch, step, n)
     room = _room(mh, kind, n)
     seed = 1760000000 + n
     with mh.Session(room, chains, seed=seed, rng=1) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -492,7 +522,7 @@ def test_oversized_room_is_rejected(mh, hiplib):
 
 # ---- parallel tempering (mh_options.n_temps > 1) ---------------------------------------------
 
-@pytest.mark.parametrize("step", ["incremental", "full"])
+@pytest.mark.parametrize("step", STEPS)
 @pytest.mark.parametrize("kind,n,K,chains,steps,interval", [
     ("main", 32, 4, 64, 300, 25),
     ("syn", 9, 2, 128, 400, 1),       # an exchange round after every step
@@ -504,11 +534,11 @@ def test_tempering_matches_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, K
                                   interval):
     """Replica exchange on the device (per-chain beta in both step kernels, mh_exchange_kernel
     between launches) against the oracle's restatement, bit for bit, outputs in rung order."""
-    monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    kind_ = _use_step(monkeypatch, step, n)
     room = _room(mh, kind, n)
     seed = 3100 + n + K
     with mh.Session(room, chains, seed=seed, temps=K, swap_interval=interval, beta_min=0.2) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
