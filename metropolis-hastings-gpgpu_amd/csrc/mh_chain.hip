@@ -153,6 +153,141 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
     rel_terms(ch.relc[q], ch.P, tpw, tang);
 }
 
+// ---- incremental Clearance pairs (one object per lane) ---------------------------------------
+//
+// A proposal changes the pairs of the moved objects' columns and of the rows of clearances they
+// carry; the others keep their zero / non-zero state. Updates this lane's column mask and the
+// proposed row words (the other LDS buffer), writes the row prefix counts of the proposed rows
+// and returns the number of non-zero pairs (Kernel.cu:408-431 terms that are not exactly zero).
+template <int L>
+__device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, int ka, int kb,
+                                             int r, int gbase, float4 boxj, const ClPairs& clp,
+                                             ClPairs& clo) {
+    const int j = r;
+    const uint64_t* NZc = ch.NZ + clp.buf * c;
+    uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
+    uint64_t cm = clp.cm;
+    uint64_t w = (r < c) ? NZc[r] : 0ull;  // lane r's clearance row, patched below
+    const int kk2[2] = {ka, kb};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // the moved objects' columns, one clearance per lane
+        const int k = kk2[q];
+        if (k < 0) continue;
+        const ObjP pk = ch.P[k];
+        const float4 bk = shape_box(ch.objs[k], pk.xf, pk.yf);
+        const bool nzk = r < c && overlap(ch.CLA[r], bk) != 0.0f;
+        const uint64_t colk = group_ballot<L>(nzk, gbase);
+        if (j == k) cm = colk;
+        w = (w & ~(1ull << k)) | ((uint64_t)nzk << k);
+    }
+    // rows of the clearances whose source moved: every object lane re-tests its pair
+    uint64_t moved = group_ballot<L>(r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb),
+                                     gbase);
+    while (moved) {
+        const int i = __builtin_ctzll(moved);
+        moved &= moved - 1;
+        const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
+        const uint64_t row = group_ballot<L>(nzi, gbase);
+        cm = (cm & ~(1ull << i)) | ((uint64_t)nzi << i);
+        if (r == i) w = row;
+    }
+    if (r < c) NZn[r] = w;
+    int total;
+    const int pre = group_excl_scan<L>(r < c ? __builtin_popcountll(w) : 0, r, total);
+    if (r < c) ch.PRE[r] = pre;
+    clo.cm = cm;
+    clo.buf = clp.buf ^ 1;
+    wave_sync();
+    return total;
+}
+
+// ---- the rejection bound ---------------------------------------------------------------------
+//
+// Accept (Kernel.cu:706-713) rejects when u >= min(1, (float)exp(BETA (star - cur))). Most
+// proposals are rejected, and a rejected proposal's costs are never used, so the exact,
+// serially replayed sums are needed only when the decision is not already certain. The bound
+// takes every term of every sum (one object, one relationship and this lane's Clearance pairs
+// per lane), sums them across the group in fp32 and bounds the distance to the reference's
+// sequential sums: a sum of n non-zero terms accumulated with rounding unit U (one rounding, or
+// a double rounding in float for the VisualBalance sums) is within n U sum|t| (1 + nU) of the
+// exact sum; the fp32 group sum is within (k + 7) U sum|t| of it (k terms summed per lane, a
+// six-level tree) -- both covered by (2n + 26) U sum|t|. The cost composition (Kernel.cu:518-549)
+// is bounded term by term with interval arithmetic (VisualBalance is 1-Lipschitz in its float
+// coordinates, PairWise a product of two sums), every float rounding counted at 2U and the
+// whole bound widened by 1.25. The decision is certain when the bound puts the upper total
+// below log(u): u >= exp(x) (1 + U) >= (float)exp(x) for every total up to that bound.
+template <int L>
+__device__ __forceinline__ float group_fsum(float v) {
+    v += bfly<1>(v);
+    v += bfly<2>(v);
+    if constexpr (L >= 8) v += bfly<4>(v);
+    if constexpr (L >= 16) v += bfly<8>(v);
+    if constexpr (L >= 32) v += bfly<16>(v);
+    if constexpr (L >= 64) v += bfly<32>(v);
+    return v;
+}
+
+template <int L>
+__device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                               double px, double py, float cph, float mx,
+                                               float4 sac, float4 sao, double rpw, double rang,
+                                               float clsum, int kcl, float u, float cur,
+                                               int gbase) {
+    constexpr float U = 0x1p-24f;
+    // this lane's terms, with the signs the reference sums them with
+    const float tnx = (float)px, tny = (float)py;
+    const float tfp = -cph, tsym = -mx, tcl = -clsum;
+    const float tsa = -((sac.x + sac.y + sac.z + sac.w) + (sao.x + sao.y + sao.z + sao.w));
+    const float tpw = -(float)rpw, tang = -(float)rang;
+    const float lfp = rm.w_fp * tfp, lsym = rm.w_sym * tsym, lcl = rm.w_cl * tcl,
+                lsa = rm.w_sa * tsa;
+    const float lin = (lfp + lsym) + (lcl + lsa);
+    const float cn = (2.0f * n + 26.0f) * U;
+    const float elin = cn * (fabsf(lfp) + fabsf(lsym)) +
+                       (2.0f * ncl + 26.0f + kcl) * U * fabsf(lcl) +
+                       (8.0f * (c + n) + 34.0f) * U * fabsf(lsa) +
+                       12.0f * U * (fabsf(lfp) + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
+    const float s_nx = group_fsum<L>(tnx), s_ny = group_fsum<L>(tny);
+    const float s_pw = group_fsum<L>(tpw), s_ang = group_fsum<L>(tang);
+    const float s_lin = group_fsum<L>(lin), s_elin = group_fsum<L>(elin);
+    // sums of |t|: equal to |sum| when no term has the other sign (the usual case)
+    float a_nx = fabsf(s_nx), a_ny = fabsf(s_ny), a_ang = fabsf(s_ang);
+    if (group_ballot<L>(tnx < 0.0f || tny < 0.0f || tang > 0.0f, gbase) != 0) {
+        a_nx = group_fsum<L>(fabsf(tnx));
+        a_ny = group_fsum<L>(fabsf(tny));
+        a_ang = group_fsum<L>(fabsf(tang));
+    }
+    const double Ud = 0x1p-24;
+    // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
+    const double den = fabs((double)rm.denom);
+    const double enx = (2.0 * n + 26.0) * Ud * a_nx / den, eny = (2.0 * n + 26.0) * Ud * a_ny / den;
+    const double ad = (double)s_nx / rm.denom, bd = (double)s_ny / rm.denom;
+    const double da = enx + 2.0 * Ud * (fabs(ad) + enx), db = eny + 2.0 * Ud * (fabs(bd) + eny);
+    const double fx = ad - (double)rm.cxf, fy = bd - (double)rm.cyf;
+    const double dfx = da + 2.0 * Ud * (fabs(fx) + da), dfy = db + 2.0 * Ud * (fabs(fy) + db);
+    const double vb = -sqrt(fx * fx + fy * fy);
+    const double dvb = dfx + dfy + 2.0 * Ud * (fabs(vb) + dfx + dfy);
+    const double o2 = (double)rm.w_vb * vb;
+    const double e2 = fabs((double)rm.w_vb) * (dvb + 3.0 * Ud * (fabs(vb) + dvb));
+    // PairWise x PairWiseAngle (Kernel.cu:518)
+    const double epw = (2.0 * nrel + 26.0) * Ud * fabs((double)s_pw);
+    const double eang = (2.0 * nrel + 26.0) * Ud * a_ang;
+    const double pa = (double)s_pw * (double)s_ang;
+    const double dpa = fabs((double)s_pw) * eang + fabs((double)s_ang) * epw + epw * eang;
+    const double o1 = (double)rm.w_pw * pa;
+    const double e1 = fabs((double)rm.w_pw) * (dpa + 3.0 * Ud * (fabs(pa) + dpa));
+    // total (Kernel.cu:547) and its upper end
+    const double t = o1 + o2 + (double)s_lin;
+    const double e = e1 + e2 + (double)s_elin + 12.0 * Ud * (fabs(o1) + e1 + fabs(o2) + e2);
+    const double thi = t + 1.25 * e;
+    const double x = kBeta * (thi - (double)cur);
+    // log(u) from the f32 log: within 1e-6 of the true value for u in [2^-33, 1]; 1e-4 margin
+    const double lu = (double)__logf(u);
+    const bool rej = (x <= lu - 1e-4) && (thi < 1e30) && (thi > -1e30);  // NaN: not certain
+    // one decision per chain: the group's first lane decides
+    return (group_ballot<L>(rej, gbase) & 1ull) != 0;
+}
+
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
@@ -160,10 +295,15 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
 // configuration. With DELTA, `prev` holds them for the configuration before the proposal, which
 // differs from the evaluated one only in objects ka and kb (-1: none), and only the rows and
 // columns those objects touch are re-evaluated.
-template <int L, int NPL, bool WITH_OL, bool DELTA>
+// FAST (steps without best-of-chain tracking, one chain per wavefront): before any ordered sum
+// is built, the proposal's total is bounded from lane-parallel sums (certain_reject) and, when
+// the bound already decides Accept's rejection for the drawn uniform `u_acc`, the function
+// returns with *fast_reject set and `out` unset; otherwise it goes on to the exact costs.
+template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false>
 __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
-                           int kb, ClPairs& clo, const ClPairs& clp) {
+                           int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
+                           float cur_total = 0.0f, bool* fast_reject = nullptr) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
     const DevRoom& rm = *ch.rm;
@@ -540,6 +680,31 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     }
 
     if (r == 0) MH_PHASE(ch, 2, t0);
+    // One object per lane: the non-zero Clearance pairs are tracked incrementally
+    // (inc_cl_update); the 8-lane instance keeps the direct pass below (with a handful of
+    // clearances its latency is lower, and those rooms run few chains).
+    constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
+    int cl_total = 0;
+    if constexpr (INC_CL) cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo);
+    if constexpr (FAST) {
+        static_assert(INC_CL && L == 64, "the rejection bound needs one chain per wavefront");
+        if (rm.r <= L) {  // every relationship term is held by a lane (rpw[0], rang[0])
+            float clsum = 0.0f;  // this lane's object against the clearances it overlaps
+            uint64_t bits = r < n ? clo.cm : 0ull;
+            const int kcl = __builtin_popcountll(bits);
+            while (bits) {
+                const int i = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                clsum += overlap(ch.CLA[i], boxo[0]);
+            }
+            if (certain_reject<L>(rm, n, c, rm.r, cl_total, px[0], py[0], cph[0], sym.mx[0],
+                                  sac[0], sao[0], rpw[0], rang[0], clsum, kcl, u_acc,
+                                  cur_total, gbase)) {
+                *fast_reject = true;
+                return;
+            }
+        }
+    }
     // The eight ordered sums of Costs() -- VisualBalance nx and ny (float through double
     // temporaries, :200-201), FocalPoint (double, :277), Symmetry (float, :314), SurfaceArea
     // (float, :463-479), Clearance (float, :429), PairWise and PairWiseAngle (double, :222,
@@ -578,64 +743,26 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     if (r == 0) MH_PHASE(ch, 4, t0);
     // ClearanceCosts pairs, clearance-major then object (Kernel.cu:408-431).
     int cnt_cl = 0;
-    // One object per lane: the non-zero pairs are tracked incrementally. A proposal changes
-    // the pairs of the moved objects' columns and of the rows of clearances they carry; the
-    // others keep their zero / non-zero state, so only the non-zero pairs are re-evaluated,
-    // each by its object's lane, and written straight to their list positions (row prefix +
-    // the row's set bits below the object).
-    // (The 8-lane instance keeps the direct pass: with a handful of clearances its latency is
-    // lower, and those rooms run few chains -- config 2 is latency-bound.)
-    constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
+    // One object per lane: only the non-zero pairs (inc_cl_update) are re-evaluated, each by its
+    // object's lane, and written straight to their list positions (row prefix + the row's set
+    // bits below the object).
     constexpr bool CL_STATE = NPL == 1 && L >= 16;  // pair state kept for the steps
     bool cl_done = false;
     if constexpr (NPL == 1) {
         const int j = r;
         const float4 boxj = boxo[0];
         if constexpr (INC_CL) {
-            const uint64_t* NZc = ch.NZ + clp.buf * c;
-            uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
-            uint64_t cm = clp.cm;
-            uint64_t w = (r < c) ? NZc[r] : 0ull;  // lane r's clearance row, patched below
-            const int kk2[2] = {ka, kb};
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {  // the moved objects' columns, one clearance per lane
-                const int k = kk2[q];
-                if (k < 0) continue;
-                const ObjP pk = ch.P[k];
-                const float4 bk = shape_box(ch.objs[k], pk.xf, pk.yf);
-                const bool nzk = r < c && overlap(ch.CLA[r], bk) != 0.0f;
-                const uint64_t colk = group_ballot<L>(nzk, gbase);
-                if (j == k) cm = colk;
-                w = (w & ~(1ull << k)) | ((uint64_t)nzk << k);
-            }
-            // rows of the clearances whose source moved: every object lane re-tests its pair
-            uint64_t moved = group_ballot<L>(r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb),
-                                             gbase);
-            while (moved) {
-                const int i = __builtin_ctzll(moved);
-                moved &= moved - 1;
-                const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
-                const uint64_t row = group_ballot<L>(nzi, gbase);
-                cm = (cm & ~(1ull << i)) | ((uint64_t)nzi << i);
-                if (r == i) w = row;
-            }
-            if (r < c) NZn[r] = w;
-            int total;
-            const int pre = group_excl_scan<L>(r < c ? __builtin_popcountll(w) : 0, r, total);
-            if (r < c) ch.PRE[r] = pre;
-            clo.cm = cm;
-            clo.buf = clp.buf ^ 1;
-            wave_sync();
-            if (total <= 2 * L) {  // fits the list: write every term at its position
+            const uint64_t* NZn = ch.NZ + clo.buf * c;
+            if (cl_total <= 2 * L) {  // fits the list: write every term at its position
                 const uint64_t below = (1ull << j) - 1ull;
-                uint64_t bits = j < n ? cm : 0ull;
+                uint64_t bits = j < n ? clo.cm : 0ull;
                 while (bits) {
                     const int i = __builtin_ctzll(bits);
                     bits &= bits - 1;
                     const int pos = ch.PRE[i] + __builtin_popcountll(NZn[i] & below);
                     ch.LCL[pos] = (double)-overlap(ch.CLA[i], boxj);
                 }
-                cnt_cl = total;
+                cnt_cl = cl_total;
                 cl_done = true;
             }
         } else if constexpr (!DELTA && CL_STATE) {
@@ -1109,7 +1236,15 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             float sc[8];
             SymRows<NPL> ss;
             ClPairs cls;
-            eval_costs<L, NPL, false, true>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y, cls, cl);
+            // Steps of plain chains, one per wavefront: Accept's uniform (the next draw after the
+            // proposal's, Kernel.cu:710) is drawn first, so a proposal the rejection bound
+            // already rejects skips the exact sums (eval_costs FAST).
+            constexpr bool FASTK = !TRACK && NPL == 1 && L == 64 && !(MH_ABLATE & 4);
+            bool fast_rej = false;
+            float u_acc = 0.0f;
+            if constexpr (FASTK) u_acc = rng.uniform();
+            eval_costs<L, NPL, false, true, FASTK>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y, cls,
+                                                    cl, u_acc, cur_total, &fast_rej);
             MH_STAMP(ts);
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if constexpr (TRACK) {
@@ -1120,6 +1255,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             }
             bool acc;
             if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
+            else if constexpr (FASTK)
+                acc = !fast_rej &&
+                      u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
             else acc = accept(rng, sc[0], cur_total);
             if (acc) {
                 cur_total = sc[0];
