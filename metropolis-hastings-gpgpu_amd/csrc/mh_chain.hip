@@ -201,93 +201,6 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
     return total;
 }
 
-// ---- the rejection bound ---------------------------------------------------------------------
-//
-// Accept (Kernel.cu:706-713) rejects when u >= min(1, (float)exp(BETA (star - cur))). Most
-// proposals are rejected, and a rejected proposal's costs are never used, so the exact,
-// serially replayed sums are needed only when the decision is not already certain. The bound
-// takes every term of every sum (one object, one relationship and this lane's Clearance pairs
-// per lane), sums them across the group in fp32 and bounds the distance to the reference's
-// sequential sums: a sum of n non-zero terms accumulated with rounding unit U (one rounding, or
-// a double rounding in float for the VisualBalance sums) is within n U sum|t| (1 + nU) of the
-// exact sum; the fp32 group sum is within (k + 7) U sum|t| of it (k terms summed per lane, a
-// six-level tree) -- both covered by (2n + 26) U sum|t|. The cost composition (Kernel.cu:518-549)
-// is bounded term by term with interval arithmetic (VisualBalance is 1-Lipschitz in its float
-// coordinates, PairWise a product of two sums), every float rounding counted at 2U and the
-// whole bound widened by 1.25. The decision is certain when the bound puts the upper total
-// below log(u): u >= exp(x) (1 + U) >= (float)exp(x) for every total up to that bound.
-template <int L>
-__device__ __forceinline__ float group_fsum(float v) {
-    v += bfly<1>(v);
-    v += bfly<2>(v);
-    if constexpr (L >= 8) v += bfly<4>(v);
-    if constexpr (L >= 16) v += bfly<8>(v);
-    if constexpr (L >= 32) v += bfly<16>(v);
-    if constexpr (L >= 64) v += bfly<32>(v);
-    return v;
-}
-
-template <int L>
-__device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
-                                               double px, double py, float cph, float mx,
-                                               float4 sac, float4 sao, double rpw, double rang,
-                                               float clsum, int kcl, float u, float cur,
-                                               int gbase) {
-    constexpr float U = 0x1p-24f;
-    // this lane's terms, with the signs the reference sums them with
-    const float tnx = (float)px, tny = (float)py;
-    const float tfp = -cph, tsym = -mx, tcl = -clsum;
-    const float tsa = -((sac.x + sac.y + sac.z + sac.w) + (sao.x + sao.y + sao.z + sao.w));
-    const float tpw = -(float)rpw, tang = -(float)rang;
-    const float lfp = rm.w_fp * tfp, lsym = rm.w_sym * tsym, lcl = rm.w_cl * tcl,
-                lsa = rm.w_sa * tsa;
-    const float lin = (lfp + lsym) + (lcl + lsa);
-    const float cn = (2.0f * n + 26.0f) * U;
-    const float elin = cn * (fabsf(lfp) + fabsf(lsym)) +
-                       (2.0f * ncl + 26.0f + kcl) * U * fabsf(lcl) +
-                       (8.0f * (c + n) + 34.0f) * U * fabsf(lsa) +
-                       12.0f * U * (fabsf(lfp) + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
-    const float s_nx = group_fsum<L>(tnx), s_ny = group_fsum<L>(tny);
-    const float s_pw = group_fsum<L>(tpw), s_ang = group_fsum<L>(tang);
-    const float s_lin = group_fsum<L>(lin), s_elin = group_fsum<L>(elin);
-    // sums of |t|: equal to |sum| when no term has the other sign (the usual case)
-    float a_nx = fabsf(s_nx), a_ny = fabsf(s_ny), a_ang = fabsf(s_ang);
-    if (group_ballot<L>(tnx < 0.0f || tny < 0.0f || tang > 0.0f, gbase) != 0) {
-        a_nx = group_fsum<L>(fabsf(tnx));
-        a_ny = group_fsum<L>(fabsf(tny));
-        a_ang = group_fsum<L>(fabsf(tang));
-    }
-    const double Ud = 0x1p-24;
-    // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
-    const double den = fabs((double)rm.denom);
-    const double enx = (2.0 * n + 26.0) * Ud * a_nx / den, eny = (2.0 * n + 26.0) * Ud * a_ny / den;
-    const double ad = (double)s_nx / rm.denom, bd = (double)s_ny / rm.denom;
-    const double da = enx + 2.0 * Ud * (fabs(ad) + enx), db = eny + 2.0 * Ud * (fabs(bd) + eny);
-    const double fx = ad - (double)rm.cxf, fy = bd - (double)rm.cyf;
-    const double dfx = da + 2.0 * Ud * (fabs(fx) + da), dfy = db + 2.0 * Ud * (fabs(fy) + db);
-    const double vb = -sqrt(fx * fx + fy * fy);
-    const double dvb = dfx + dfy + 2.0 * Ud * (fabs(vb) + dfx + dfy);
-    const double o2 = (double)rm.w_vb * vb;
-    const double e2 = fabs((double)rm.w_vb) * (dvb + 3.0 * Ud * (fabs(vb) + dvb));
-    // PairWise x PairWiseAngle (Kernel.cu:518)
-    const double epw = (2.0 * nrel + 26.0) * Ud * fabs((double)s_pw);
-    const double eang = (2.0 * nrel + 26.0) * Ud * a_ang;
-    const double pa = (double)s_pw * (double)s_ang;
-    const double dpa = fabs((double)s_pw) * eang + fabs((double)s_ang) * epw + epw * eang;
-    const double o1 = (double)rm.w_pw * pa;
-    const double e1 = fabs((double)rm.w_pw) * (dpa + 3.0 * Ud * (fabs(pa) + dpa));
-    // total (Kernel.cu:547) and its upper end
-    const double t = o1 + o2 + (double)s_lin;
-    const double e = e1 + e2 + (double)s_elin + 12.0 * Ud * (fabs(o1) + e1 + fabs(o2) + e2);
-    const double thi = t + 1.25 * e;
-    const double x = kBeta * (thi - (double)cur);
-    // log(u) from the f32 log: within 1e-6 of the true value for u in [2^-33, 1]; 1e-4 margin
-    const double lu = (double)__logf(u);
-    const bool rej = (x <= lu - 1e-4) && (thi < 1e30) && (thi > -1e30);  // NaN: not certain
-    // one decision per chain: the group's first lane decides
-    return (group_ballot<L>(rej, gbase) & 1ull) != 0;
-}
-
 // ---- Costs(), Kernel.cu:516-550, for the configuration currently in LDS --------------------
 //
 // Every lane of the group returns the same costs. out: resultCosts order
@@ -686,6 +599,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
     int cl_total = 0;
     if constexpr (INC_CL) cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo);
+    if (r == 0) MH_PHASE(ch, 3, t0);
     if constexpr (FAST) {
         static_assert(INC_CL && L == 64, "the rejection bound needs one chain per wavefront");
         if (rm.r <= L) {  // every relationship term is held by a lane (rpw[0], rang[0])
@@ -697,9 +611,26 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 bits &= bits - 1;
                 clsum += overlap(ch.CLA[i], boxo[0]);
             }
-            if (certain_reject<L>(rm, n, c, rm.r, cl_total, px[0], py[0], cph[0], sym.mx[0],
-                                  sac[0], sao[0], rpw[0], rang[0], clsum, kcl, u_acc,
-                                  cur_total, gbase)) {
+            BoundTerms bt;
+            bt.nx = (float)px[0];
+            bt.ny = (float)py[0];
+            bt.anx = fabsf(bt.nx);
+            bt.any = fabsf(bt.ny);
+            bt.fp = -cph[0];
+            bt.afp = fabsf(bt.fp);
+            bt.sym = -sym.mx[0];
+            bt.cl = -clsum;
+            bt.kcl = kcl;
+            bt.sa = -((sac[0].x + sac[0].y + sac[0].z + sac[0].w) +
+                      (sao[0].x + sao[0].y + sao[0].z + sao[0].w));
+            bt.pw = -(float)rpw[0];
+            bt.ang = -(float)rang[0];
+            bt.aang = fabsf(bt.ang);
+            bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
+            const bool rej = certain_reject<L>(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total,
+                                               gbase);
+            if (r == 0) MH_PHASE(ch, 4, t0);
+            if (rej) {
                 *fast_reject = true;
                 return;
             }
@@ -713,7 +644,6 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     // (x - 0 == x, so dropping exact zeros is exact). Each step is rn_d(acc + v) with v the
     // negated term where the reference subtracts, rounded on to float for the float
     // accumulators (rn_f(rn_d(a + b)) == rn_f(a + b) for floats: 53 >= 2*24 + 2 bits).
-    if (r == 0) MH_PHASE(ch, 3, t0);
     double acc = 0.0;  // lane k of the group owns sum k (k = 5 unused; SurfaceArea below)
     const bool acc_float = (r == 0 || r == 1 || r == 3 || r == 4);
 #pragma unroll
@@ -740,7 +670,6 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         if (m * L < n) sa = serial_sub4<L>(sa, sao[m], gbase);
     }
 
-    if (r == 0) MH_PHASE(ch, 4, t0);
     // ClearanceCosts pairs, clearance-major then object (Kernel.cu:408-431).
     int cnt_cl = 0;
     // One object per lane: only the non-zero pairs (inc_cl_update) are re-evaluated, each by its
@@ -831,7 +760,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     }
     }
 
-    if (r == 0) MH_PHASE(ch, 5, t0);
+    if (r == 0) MH_PHASE(ch, 5, t0);  // SurfaceArea walk and Clearance list
     // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms.
     int cnt_pw = 0, cnt_ang = 0;
     for (int rep = 0; rep < MH_REPS(16); ++rep) {

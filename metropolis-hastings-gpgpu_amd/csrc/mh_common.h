@@ -620,6 +620,104 @@ __device__ __forceinline__ T sel(const T (&a)[NPL], int m) {
     return v;
 }
 
+// ---- the rejection bound ---------------------------------------------------------------------
+//
+// Accept (Kernel.cu:706-713) rejects when u >= min(1, (float)exp(BETA (star - cur))). Most
+// proposals are rejected, and a rejected proposal's costs are never used, so the exact,
+// serially replayed sums are needed only when the decision is not already certain. The bound
+// takes every term of every sum (each lane pre-sums the terms it holds), sums them across the
+// chain's lanes in fp32 and bounds the distance to the reference's sequential sums: a sum of n
+// non-zero terms accumulated with rounding unit U (one rounding, or a double rounding in float
+// for the VisualBalance sums) is within n U sum|t| (1 + nU) of the exact sum; the fp32 group
+// sum is within (k + 7) U sum|t| of it (k terms pre-summed per lane, a six-level tree, the
+// conversion of double terms) -- all covered by (2n + 26 + k) U sum|t|. The cost composition
+// (Kernel.cu:518-549) is bounded term by term with interval arithmetic (VisualBalance is
+// 1-Lipschitz in its float coordinates, PairWise a product of two sums), every float rounding
+// counted at 2U or more and the whole bound widened by 1.25. The decision is certain when the
+// bound puts the upper total's exponent below log(u): u >= exp(x) (1 + U) >= (float)exp(x) for
+// every total up to that bound.
+
+// One lane's partial sums of the terms of Costs() for the bound, signed as the reference sums
+// them; a* are partial sums of |term| where terms of both signs can occur.
+struct BoundTerms {
+    float nx, ny, anx, any;  // VisualBalance area * x, area * y (Kernel.cu:200-201)
+    float fp, afp;           // FocalPoint -cos(phi) (:277)
+    float sym;               // Symmetry -(row max) (:314), all <= 0
+    float cl;                // Clearance -overlap (:429), all <= 0
+    int kcl;                 // Clearance terms pre-summed by this lane
+    float sa;                // SurfaceArea -overlap (:463-479), all <= 0
+    float pw, ang, aang;     // PairWise -(range term) (<= 0), PairWiseAngle (:222, :249-253)
+    int k;                   // most terms pre-summed into any other partial sum
+};
+
+template <int L>
+__device__ __forceinline__ float group_fsum(float v) {
+    v += bfly<1>(v);
+    v += bfly<2>(v);
+    if constexpr (L >= 8) v += bfly<4>(v);
+    if constexpr (L >= 16) v += bfly<8>(v);
+    if constexpr (L >= 32) v += bfly<16>(v);
+    if constexpr (L >= 64) v += bfly<32>(v);
+    return v;
+}
+
+// Whether Accept certainly rejects this proposal (one decision per chain: the group's first
+// lane decides). n objects, c clearances, nrel relationships, ncl non-zero Clearance terms.
+template <int L>
+__device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                               const BoundTerms& bt, float u, float cur,
+                                               int gbase) {
+    constexpr float U = 0x1p-24f;
+    const float kf = (float)bt.k;
+    const float lfp = rm.w_fp * bt.fp, lsym = rm.w_sym * bt.sym, lcl = rm.w_cl * bt.cl,
+                lsa = rm.w_sa * bt.sa;
+    const float lin = (lfp + lsym) + (lcl + lsa);
+    const float cn = (2.0f * n + 26.0f + kf) * U;
+    const float elin = cn * (fabsf(rm.w_fp) * bt.afp + fabsf(lsym)) +
+                       (2.0f * ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
+                       (8.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
+                       12.0f * U * (fabsf(rm.w_fp) * bt.afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
+    const float s_nx = group_fsum<L>(bt.nx), s_ny = group_fsum<L>(bt.ny);
+    const float s_pw = group_fsum<L>(bt.pw), s_ang = group_fsum<L>(bt.ang);
+    const float s_lin = group_fsum<L>(lin), s_elin = group_fsum<L>(elin);
+    // sums of |t|: equal to |sum| when no lane holds a term of the other sign (the usual case)
+    float a_nx = fabsf(s_nx), a_ny = fabsf(s_ny), a_ang = fabsf(s_ang);
+    if (group_ballot<L>(bt.anx != bt.nx || bt.any != bt.ny || bt.aang != -bt.ang, gbase) != 0) {
+        a_nx = group_fsum<L>(bt.anx);
+        a_ny = group_fsum<L>(bt.any);
+        a_ang = group_fsum<L>(bt.aang);
+    }
+    const double Ud = 0x1p-24;
+    // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
+    const double den = fabs((double)rm.denom);
+    const double cv = (2.0 * n + 26.0 + kf) * Ud;
+    const double enx = cv * a_nx / den, eny = cv * a_ny / den;
+    const double ad = (double)s_nx / rm.denom, bd = (double)s_ny / rm.denom;
+    const double da = enx + 2.0 * Ud * (fabs(ad) + enx), db = eny + 2.0 * Ud * (fabs(bd) + eny);
+    const double fx = ad - (double)rm.cxf, fy = bd - (double)rm.cyf;
+    const double dfx = da + 2.0 * Ud * (fabs(fx) + da), dfy = db + 2.0 * Ud * (fabs(fy) + db);
+    const double vb = -sqrt(fx * fx + fy * fy);
+    const double dvb = dfx + dfy + 2.0 * Ud * (fabs(vb) + dfx + dfy);
+    const double o2 = (double)rm.w_vb * vb;
+    const double e2 = fabs((double)rm.w_vb) * (dvb + 3.0 * Ud * (fabs(vb) + dvb));
+    // PairWise x PairWiseAngle (Kernel.cu:518)
+    const double cr = (2.0 * nrel + 26.0 + kf) * Ud;
+    const double epw = cr * fabs((double)s_pw), eang = cr * a_ang;
+    const double pa = (double)s_pw * (double)s_ang;
+    const double dpa = fabs((double)s_pw) * eang + fabs((double)s_ang) * epw + epw * eang;
+    const double o1 = (double)rm.w_pw * pa;
+    const double e1 = fabs((double)rm.w_pw) * (dpa + 3.0 * Ud * (fabs(pa) + dpa));
+    // total (Kernel.cu:547) and its upper end
+    const double t = o1 + o2 + (double)s_lin;
+    const double e = e1 + e2 + (double)s_elin + 12.0 * Ud * (fabs(o1) + e1 + fabs(o2) + e2);
+    const double thi = t + 1.25 * e;
+    const double x = kBeta * (thi - (double)cur);
+    // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
+    const double lu = (double)__logf(u);
+    const bool rej = (x <= lu - 1e-4) && (thi < 1e30) && (thi > -1e30);  // NaN: not certain
+    return (group_ballot<L>(rej, gbase) & 1ull) != 0;
+}
+
 // Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that
 // attains each (-1: the 0 floor of Kernel.cu:303 is the maximum).
 template <int NPL>

@@ -418,6 +418,63 @@ __device__ int build_sa_list(const DeltaPtrs& ch, int n, int c, int r, int lo) {
     return base;
 }
 
+// ---- terms for the rejection bound (certain_reject, mh_common.h) --------------------------
+
+// This lane's partial sums of every term of Costs() for the configuration in LDS: its objects
+// (VisualBalance, FocalPoint, Symmetry rows in `nmx`), its relationships, its clearances' non-zero
+// pairs and its SurfaceArea entries. `ncl` returns the chain's count of non-zero Clearance terms.
+template <int L>
+__device__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, int n, int c, int nr,
+                                        const float* nmx, int r, int& ncl) {
+    BoundTerms bt;
+    bt.nx = bt.ny = bt.anx = bt.any = bt.fp = bt.afp = bt.sym = bt.cl = bt.sa = 0.0f;
+    bt.pw = bt.ang = bt.aang = 0.0f;
+    int kd = 0;
+    for (int i = r; i < n; i += L, ++kd) {
+        const float a = ch.AREA[i];
+        const float tx = (float)((double)a * ch.X[i]), ty = (float)((double)a * ch.Y[i]);
+        bt.nx += tx;
+        bt.ny += ty;
+        bt.anx += fabsf(tx);
+        bt.any += fabsf(ty);
+        bt.fp += ch.CPH[i];
+        bt.afp += fabsf(ch.CPH[i]);
+        bt.sym += nmx[i];
+    }
+    int kr = 0;
+    for (int q = r; q < nr; q += L, ++kr) {
+        const float tp = (float)ch.RPW[q], ta = (float)ch.RANG[q];
+        bt.pw += tp;
+        bt.ang += ta;
+        bt.aang += fabsf(ta);
+    }
+    int kcl = 0;
+    for (int ci = r; ci < c; ci += L) {
+        const float4 A = ch.CLA[ci];
+        for (int w = 0; w < ch.W; ++w) {
+            uint64_t word = ch.NZ[ci * ch.W + w];
+            while (word) {
+                const int j = w * 64 + __builtin_ctzll(word);
+                word &= word - 1;
+                bt.cl -= overlap(A, obj_box(ch, j));
+                ++kcl;
+            }
+        }
+    }
+    int ksa = 0;
+    for (int e = r; e < c + n; e += L) {
+        if ((ch.SAM[e >> 5] >> (e & 31)) & 1u) {
+            const float4 v = sa_entry(ch, c, e);
+            bt.sa -= (v.x + v.y) + (v.z + v.w);
+            ksa += 4;
+        }
+    }
+    bt.kcl = kcl;
+    bt.k = max(max(kd, kr), ksa);
+    ncl = group_sum<L>(kcl);
+    return bt;
+}
+
 // ---- proposal (propose(), Kernel.cu:566-704) in place ---------------------------------------
 
 __device__ __forceinline__ DBackup read_obj(const DeltaPtrs& ch, int k) {
@@ -829,6 +886,20 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
         symmetry_delta<L>(ch, n, cur, nxt, ka, kb, wild_star > 0, r, gbase);
         wave_sync();
         DSTAMP(3);
+        // Plain chains, one per wavefront: Accept's uniform (the next draw after the proposal's,
+        // Kernel.cu:710) is drawn first, and a proposal the rejection bound already rejects
+        // skips the term lists and the replay.
+        constexpr bool FASTD = !TRACK && L == 64;
+        bool fast_rej = false;
+        float u_acc = 0.0f;
+        if constexpr (FASTD) {
+            u_acc = rng.uniform();
+            int ncl;
+            const BoundTerms bt = delta_bound_terms<L>(ch, n, c, nr, nxt.nmx, r, ncl);
+            fast_rej = certain_reject<L>(*rm_l, n, c, nr, ncl, bt, u_acc, cur_total, gbase);
+        }
+        float sc[8];
+        if (!fast_rej) {
         const int cnt_cl = build_cl_list<L>(ch, c, r, 0);
         const int cnt_sa = build_sa_list<L>(ch, n, c, r, 0);
         // zero past each list's end: to NP for the dense walk, to round4 for the list walk
@@ -846,9 +917,9 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
             atomicAdd(&g_delta_counts[3], (unsigned long long)(cnt_sa > ch.cap_sa));
         }
 #endif
-        float sc[8];
         replay<L>(ch, n, nxt.nmx, cnt_cl, cnt_sa, r, gbase, sc);
         DSTAMP(5);
+        }
         // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
         if constexpr (TRACK) {
             if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
@@ -858,6 +929,9 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
         }
         bool acc;
         if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
+        else if constexpr (FASTD)
+            acc = !fast_rej &&
+                  u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
         else acc = accept(rng, sc[0], cur_total);
         if (acc) {
             cur_total = sc[0];

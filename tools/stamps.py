@@ -15,8 +15,8 @@ import __graft_entry__ as graft  # noqa: E402
 
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "term lists", "replay", "accept/restore", "-"]
-PHASES = ["propose", "A per-object", "B symmetry", "C ordered sums", "D surface area",
-          "E clearance", "F pairwise/angle", "accept/undo"]
+PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
+          "E SA walk + CL list", "F PW/ANG + replay", "accept/undo"]
 
 
 def main():
@@ -29,9 +29,9 @@ def main():
         s.run(iters)
         s.finalize()
         s.summary()
-        lanes, cpw = s.geometry()
+        lanes, cpw, s_kind = s.step_kernel()
     out = (C.c_ulonglong * 12)()
-    delta = hasattr(lib, "mh_debug_delta_cycles") and os.environ.get("MH_DELTA", "1") != "0" and n > 8
+    delta = hasattr(lib, "mh_debug_delta_cycles") and s_kind == "incremental"
     if delta:  # incremental step kernel: per-wavefront stamps, 64/lanes chains per wavefront
         assert lib.mh_debug_delta_cycles(out) == 0
         names, per = DELTA_PHASES, chains * iters / (64 // lanes)
