@@ -182,6 +182,7 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
         denom = denom + o.area;  // Kernel.cu:202, same order
     }
     rm.denom = denom;
+    rm.inv_denom = 1.0f / denom;
     out.clr.resize(c > 0 ? c : 1);
     for (int i = 0; i < c; ++i) {
         out.clr[i].shape = make_shape(vertices + clearances[i].point1Index);

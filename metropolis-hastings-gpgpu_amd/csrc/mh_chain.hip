@@ -627,8 +627,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             bt.ang = -(float)rang[0];
             bt.aang = fabsf(bt.ang);
             bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
-            const bool rej = certain_reject<L>(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total,
-                                               gbase);
+            const bool rej = certain_reject(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total);
             if (r == 0) MH_PHASE(ch, 4, t0);
             if (rej) {
                 *fast_reject = true;

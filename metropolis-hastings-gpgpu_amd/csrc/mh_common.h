@@ -650,72 +650,74 @@ struct BoundTerms {
     int k;                   // most terms pre-summed into any other partial sum
 };
 
-template <int L>
-__device__ __forceinline__ float group_fsum(float v) {
-    v += bfly<1>(v);
-    v += bfly<2>(v);
-    if constexpr (L >= 8) v += bfly<4>(v);
-    if constexpr (L >= 16) v += bfly<8>(v);
-    if constexpr (L >= 32) v += bfly<16>(v);
-    if constexpr (L >= 64) v += bfly<32>(v);
-    return v;
+// Sum of v over the 64 lanes of the wavefront, uniform (an SGPR): in-row butterflies (DPP
+// quad_perm, row_half_mirror, row_mirror), then row_bcast15 / row_bcast31 carry the row sums
+// into lane 63. The order is fixed, and the bound below counts six roundings per sum.
+__device__ __forceinline__ float wave_fsum(float v) {
+    v += __int_as_float(dpp_mov<0xB1>(__float_as_int(v)));   // quad_perm [1, 0, 3, 2]
+    v += __int_as_float(dpp_mov<0x4E>(__float_as_int(v)));   // quad_perm [2, 3, 0, 1]
+    v += __int_as_float(dpp_mov<0x141>(__float_as_int(v)));  // row_half_mirror
+    v += __int_as_float(dpp_mov<0x140>(__float_as_int(v)));  // row_mirror
+    v += __int_as_float(dpp_mov<0x142, 0xA, 0xF, false>(__float_as_int(v), 0));  // row_bcast15
+    v += __int_as_float(dpp_mov<0x143, 0xC, 0xF, false>(__float_as_int(v), 0));  // row_bcast31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-// Whether Accept certainly rejects this proposal (one decision per chain: the group's first
-// lane decides). n objects, c clearances, nrel relationships, ncl non-zero Clearance terms.
-template <int L>
+// Whether Accept certainly rejects this proposal, for a chain that owns the wavefront. n
+// objects, c clearances, nrel relationships, ncl non-zero Clearance terms. The arithmetic after
+// the lane sums is fp32 on wave-uniform values; every intermediate has at most ~30 roundings
+// on quantities no larger than M (below), so 64 U M covers them.
 __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
-                                               const BoundTerms& bt, float u, float cur,
-                                               int gbase) {
+                                               const BoundTerms& bt, float u, float cur) {
     constexpr float U = 0x1p-24f;
     const float kf = (float)bt.k;
     const float lfp = rm.w_fp * bt.fp, lsym = rm.w_sym * bt.sym, lcl = rm.w_cl * bt.cl,
                 lsa = rm.w_sa * bt.sa;
     const float lin = (lfp + lsym) + (lcl + lsa);
-    const float cn = (2.0f * n + 26.0f + kf) * U;
-    const float elin = cn * (fabsf(rm.w_fp) * bt.afp + fabsf(lsym)) +
+    const float afp = fabsf(rm.w_fp) * bt.afp;
+    const float elin = (2.0f * n + 26.0f + kf) * U * (afp + fabsf(lsym)) +
                        (2.0f * ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
                        (8.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
-                       12.0f * U * (fabsf(rm.w_fp) * bt.afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
-    const float s_nx = group_fsum<L>(bt.nx), s_ny = group_fsum<L>(bt.ny);
-    const float s_pw = group_fsum<L>(bt.pw), s_ang = group_fsum<L>(bt.ang);
-    const float s_lin = group_fsum<L>(lin), s_elin = group_fsum<L>(elin);
+                       12.0f * U * (afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
+    const float s_nx = wave_fsum(bt.nx), s_ny = wave_fsum(bt.ny);
+    const float s_pw = wave_fsum(bt.pw), s_ang = wave_fsum(bt.ang);
+    const float s_lin = wave_fsum(lin), s_elin = wave_fsum(elin);
     // sums of |t|: equal to |sum| when no lane holds a term of the other sign (the usual case)
     float a_nx = fabsf(s_nx), a_ny = fabsf(s_ny), a_ang = fabsf(s_ang);
-    if (group_ballot<L>(bt.anx != bt.nx || bt.any != bt.ny || bt.aang != -bt.ang, gbase) != 0) {
-        a_nx = group_fsum<L>(bt.anx);
-        a_ny = group_fsum<L>(bt.any);
-        a_ang = group_fsum<L>(bt.aang);
+    if (__ballot(bt.anx != bt.nx || bt.any != bt.ny || bt.aang != -bt.ang) != 0) {
+        a_nx = wave_fsum(bt.anx);
+        a_ny = wave_fsum(bt.any);
+        a_ang = wave_fsum(bt.aang);
     }
-    const double Ud = 0x1p-24;
     // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
-    const double den = fabs((double)rm.denom);
-    const double cv = (2.0 * n + 26.0 + kf) * Ud;
-    const double enx = cv * a_nx / den, eny = cv * a_ny / den;
-    const double ad = (double)s_nx / rm.denom, bd = (double)s_ny / rm.denom;
-    const double da = enx + 2.0 * Ud * (fabs(ad) + enx), db = eny + 2.0 * Ud * (fabs(bd) + eny);
-    const double fx = ad - (double)rm.cxf, fy = bd - (double)rm.cyf;
-    const double dfx = da + 2.0 * Ud * (fabs(fx) + da), dfy = db + 2.0 * Ud * (fabs(fy) + db);
-    const double vb = -sqrt(fx * fx + fy * fy);
-    const double dvb = dfx + dfy + 2.0 * Ud * (fabs(vb) + dfx + dfy);
-    const double o2 = (double)rm.w_vb * vb;
-    const double e2 = fabs((double)rm.w_vb) * (dvb + 3.0 * Ud * (fabs(vb) + dvb));
+    const float id = fabsf(rm.inv_denom);
+    const float cv = (2.0f * n + 26.0f + kf) * U;
+    const float enx = cv * a_nx * id, eny = cv * a_ny * id;
+    const float ad = s_nx * rm.inv_denom, bd = s_ny * rm.inv_denom;
+    const float da = enx + 3.0f * U * (fabsf(ad) + enx), db = eny + 3.0f * U * (fabsf(bd) + eny);
+    const float fx = ad - rm.cxf, fy = bd - rm.cyf;
+    const float dfx = da + 2.0f * U * (fabsf(fx) + da), dfy = db + 2.0f * U * (fabsf(fy) + db);
+    const float vb = -__builtin_sqrtf(fx * fx + fy * fy);
+    const float dvb = dfx + dfy + 2.0f * U * (fabsf(vb) + dfx + dfy);
+    const float o2 = rm.w_vb * vb;
+    const float e2 = fabsf(rm.w_vb) * (dvb + 3.0f * U * (fabsf(vb) + dvb));
     // PairWise x PairWiseAngle (Kernel.cu:518)
-    const double cr = (2.0 * nrel + 26.0 + kf) * Ud;
-    const double epw = cr * fabs((double)s_pw), eang = cr * a_ang;
-    const double pa = (double)s_pw * (double)s_ang;
-    const double dpa = fabs((double)s_pw) * eang + fabs((double)s_ang) * epw + epw * eang;
-    const double o1 = (double)rm.w_pw * pa;
-    const double e1 = fabs((double)rm.w_pw) * (dpa + 3.0 * Ud * (fabs(pa) + dpa));
+    const float cr = (2.0f * nrel + 26.0f + kf) * U;
+    const float epw = cr * fabsf(s_pw), eang = cr * a_ang;
+    const float pa = s_pw * s_ang;
+    const float dpa = fabsf(s_pw) * eang + fabsf(s_ang) * epw + epw * eang;
+    const float o1 = rm.w_pw * pa;
+    const float e1 = fabsf(rm.w_pw) * (dpa + 3.0f * U * (fabsf(pa) + dpa));
     // total (Kernel.cu:547) and its upper end
-    const double t = o1 + o2 + (double)s_lin;
-    const double e = e1 + e2 + (double)s_elin + 12.0 * Ud * (fabs(o1) + e1 + fabs(o2) + e2);
-    const double thi = t + 1.25 * e;
-    const double x = kBeta * (thi - (double)cur);
+    const float t = (o1 + o2) + s_lin;
+    const float m = fabsf(o1) + fabsf(o2) + fabsf(s_lin) + e1 + e2 + s_elin + fabsf(cur) +
+                    fabsf(vb) + fabsf(fx) + fabsf(fy) + fabsf(rm.w_pw) * fabsf(pa);
+    const float e = e1 + e2 + s_elin + 12.0f * U * (fabsf(o1) + e1 + fabsf(o2) + e2) + 64.0f * U * m;
+    const float x = (float)kBeta * ((t + 1.25f * e) - cur);
     // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
-    const double lu = (double)__logf(u);
-    const bool rej = (x <= lu - 1e-4) && (thi < 1e30) && (thi > -1e30);  // NaN: not certain
-    return (group_ballot<L>(rej, gbase) & 1ull) != 0;
+    const float lu = __logf(u);
+    // x <= lu - 1e-4 (the uniform compare NaN-false: an invalid bound is never certain)
+    return x <= lu - 1e-4f && x > -1e30f;
 }
 
 // Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that

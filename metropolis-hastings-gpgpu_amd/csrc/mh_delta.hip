@@ -896,7 +896,7 @@ __global__ void __launch_bounds__(512) mh_delta_kernel(LaunchArgs a) {
             u_acc = rng.uniform();
             int ncl;
             const BoundTerms bt = delta_bound_terms<L>(ch, n, c, nr, nxt.nmx, r, ncl);
-            fast_rej = certain_reject<L>(*rm_l, n, c, nr, ncl, bt, u_acc, cur_total, gbase);
+            fast_rej = certain_reject(*rm_l, n, c, nr, ncl, bt, u_acc, cur_total);
         }
         float sc[8];
         if (!fast_rej) {

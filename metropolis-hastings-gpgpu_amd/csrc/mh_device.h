@@ -65,7 +65,7 @@ struct DevRoom {
     float cxf, cyf;    // (float)(centroidX / 2), (float)(centroidY / 2), Kernel.cu:206
     float denom;       // sequential float sum of areas, Kernel.cu:202
     float sx, sy;      // proposal std devs width/16, height/16, Kernel.cu:587-591
-    float pad1;
+    float inv_denom;   // 1 / denom rounded to float (the rejection bound only)
     double along_f;        // focalX*ux + focalY*uy, Kernel.cu:292
     double two_focal_rot;  // 2 * focalRot, Kernel.cu:297
     double rmin_x, rmin_y, rmax_x, rmax_y;  // room box for the translate clamp, Kernel.cu:613-630
