@@ -647,7 +647,8 @@ struct BoundTerms {
     int kcl;                 // Clearance terms pre-summed by this lane
     float sa;                // SurfaceArea -overlap (:463-479), all <= 0
     float pw, ang, aang;     // PairWise -(range term) (<= 0), PairWiseAngle (:222, :249-253)
-    int k;                   // most terms pre-summed into any other partial sum
+    int k;                   // most terms any lane pre-sums into any other partial sum (the
+                             // same value on every lane: it enters the uniform bound)
 };
 
 // Sum of v over the 64 lanes of the wavefront, uniform (an SGPR): in-row butterflies (DPP
@@ -716,8 +717,10 @@ __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, 
     const float x = (float)kBeta * ((t + 1.25f * e) - cur);
     // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
     const float lu = __logf(u);
-    // x <= lu - 1e-4 (the uniform compare NaN-false: an invalid bound is never certain)
-    return x <= lu - 1e-4f && x > -1e30f;
+    // x <= lu - 1e-4 (the uniform compare NaN-false: an invalid bound is never certain); the
+    // chain's first lane decides, so the decision is wave-uniform by construction
+    const bool rej = x <= lu - 1e-4f && x > -1e30f;
+    return __builtin_amdgcn_readfirstlane(rej ? 1 : 0) != 0;
 }
 
 // Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that

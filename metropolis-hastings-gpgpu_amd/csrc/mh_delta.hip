@@ -429,8 +429,7 @@ __device__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, int n, int c, int n
     BoundTerms bt;
     bt.nx = bt.ny = bt.anx = bt.any = bt.fp = bt.afp = bt.sym = bt.cl = bt.sa = 0.0f;
     bt.pw = bt.ang = bt.aang = 0.0f;
-    int kd = 0;
-    for (int i = r; i < n; i += L, ++kd) {
+    for (int i = r; i < n; i += L) {
         const float a = ch.AREA[i];
         const float tx = (float)((double)a * ch.X[i]), ty = (float)((double)a * ch.Y[i]);
         bt.nx += tx;
@@ -441,8 +440,7 @@ __device__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, int n, int c, int n
         bt.afp += fabsf(ch.CPH[i]);
         bt.sym += nmx[i];
     }
-    int kr = 0;
-    for (int q = r; q < nr; q += L, ++kr) {
+    for (int q = r; q < nr; q += L) {
         const float tp = (float)ch.RPW[q], ta = (float)ch.RANG[q];
         bt.pw += tp;
         bt.ang += ta;
@@ -461,16 +459,14 @@ __device__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, int n, int c, int n
             }
         }
     }
-    int ksa = 0;
     for (int e = r; e < c + n; e += L) {
         if ((ch.SAM[e >> 5] >> (e & 31)) & 1u) {
             const float4 v = sa_entry(ch, c, e);
             bt.sa -= (v.x + v.y) + (v.z + v.w);
-            ksa += 4;
         }
     }
     bt.kcl = kcl;
-    bt.k = max(max(kd, kr), ksa);
+    bt.k = max(max((n + L - 1) / L, (nr + L - 1) / L), 4 * ((c + n + L - 1) / L));  // uniform
     ncl = group_sum<L>(kcl);
     return bt;
 }

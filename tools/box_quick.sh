@@ -6,7 +6,8 @@ TAG=${1:-quick}; K=${2:-}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread \
+timeout -k 10 120 python -u tools/canary.py || { echo "canary failed: stopping"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 170 --timeout-method thread \
     -p no:cacheprovider "${KARG[@]}" > $OUT/pytest_gpu.log 2>&1; rc=$?
 tail -6 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || { echo "pytest ended with $rc: stopping"; grep -E "Error|assert|FAILED" $OUT/pytest_gpu.log | head -20; exit $rc; }
