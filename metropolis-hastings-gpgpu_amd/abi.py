@@ -307,14 +307,14 @@ def debug_collectives(L: int, v, iv):
     lib = load_library()
     v = np.ascontiguousarray(v, dtype=np.float32)
     iv = np.ascontiguousarray(iv, dtype=np.int32)
-    out = np.zeros(9 * 64, dtype=np.int32)
+    out = np.zeros(17 * 64, dtype=np.int32)
     if lib.mh_debug_collectives(L, v.ctypes.data_as(P(C.c_float)), iv.ctypes.data_as(P(C.c_int)),
                                 out.ctypes.data_as(P(C.c_int))) != 0:
         raise MHError(last_error(lib))
-    out = out.reshape(9, 64)
+    out = out.reshape(17, 64)
     return {"m1": out[0].view(np.float32), "m2": out[1].view(np.float32), "j1": out[2],
             "max": out[3].view(np.float32), "arg": out[4], "scan": out[5], "total": out[6],
-            "imax": out[7], "isum": out[8]}
+            "imax": out[7], "isum": out[8], "wsum8": out[9:17].view(np.float32)}
 
 
 class Session:

@@ -913,12 +913,12 @@ MH_API int mh_debug_collectives(int L, const float* v, const int* iv, int* out) 
     int *d_iv = nullptr, *d_out = nullptr;
     hipError_t e = hipMalloc((void**)&d_v, sizeof(float) * 64);
     if (e == hipSuccess) e = hipMalloc((void**)&d_iv, sizeof(int) * 64);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_out, sizeof(int) * 9 * 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_out, sizeof(int) * 17 * 64);
     if (e == hipSuccess) e = hipMemcpy(d_v, v, sizeof(float) * 64, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_iv, iv, sizeof(int) * 64, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = mh::launch_collectives(L, d_v, d_iv, d_out, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(int) * 9 * 64, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(int) * 17 * 64, hipMemcpyDeviceToHost);
     (void)hipFree(d_v);
     (void)hipFree(d_iv);
     (void)hipFree(d_out);

@@ -61,7 +61,8 @@ struct ChainAux {
     int swap_a, swap_b;  // a swap proposal's objects (-1: none); z/rotX/rotZ swap in HBM on accept
     float cur[8]; // resultCosts of the current configuration
 #if MH_STAMPS
-    unsigned long long cyc[8];  // diagnostic: cycles per phase (writer lane)
+    unsigned long long cyc[10];  // diagnostic: cycles per phase (writer lane); [8] steps that
+                                 // evaluated the rejection bound, [9] steps it rejected
 #endif
 };
 static_assert(sizeof(ChainAux) <= kChainAuxBytes, "ChainAux");
@@ -629,6 +630,12 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
             const bool rej = certain_reject(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total);
             if (r == 0) MH_PHASE(ch, 4, t0);
+#if MH_STAMPS
+            if (r == 0) {
+                ch.aux->cyc[8] += 1;
+                ch.aux->cyc[9] += rej ? 1 : 0;
+            }
+#endif
             if (rej) {
                 *fast_reject = true;
                 return;
@@ -1151,7 +1158,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, cl, cl);
 #if MH_STAMPS
         if (writer)
-            for (int k = 0; k < 8; ++k) ch.aux->cyc[k] = 0;
+            for (int k = 0; k < 10; ++k) ch.aux->cyc[k] = 0;
 #endif
 #pragma clang loop unroll(disable)
         for (int it = 0; it < a.iterations; ++it) {
@@ -1204,7 +1211,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         }
 #if MH_STAMPS
         if (writer)
-            for (int k = 0; k < 8; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
+            for (int k = 0; k < 10; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
 #endif
         if (writer) {
             ChainMeta m;
@@ -1430,7 +1437,8 @@ __global__ void __launch_bounds__(256) mh_exchange_kernel(LaunchArgs a, int* per
 
 // out[k * 64 + lane] for k = 0 top-2 m1, 1 m2, 2 argmax (lane index within the group, values
 // v), 3 max-with-index value, 4 its index, 5 exclusive scan of iv, 6 its group total,
-// 7 group max of iv, 8 group sum of iv (floats as bits).
+// 7 group max of iv, 8 group sum of iv (floats as bits), 9..16 the eight wavefront sums of
+// wave_fsum8 over the lane values (float)(iv[(3 lane + k) & 63] + k), k = 0..7 (floats as bits).
 template <int L>
 __global__ void mh_collectives_kernel(const float* v, const int* iv, int* out) {
     const int lane = threadIdx.x;
@@ -1452,6 +1460,12 @@ __global__ void mh_collectives_kernel(const float* v, const int* iv, int* out) {
     out[6 * 64 + lane] = tot;
     out[7 * 64 + lane] = group_max<L>(iv[lane]);
     out[8 * 64 + lane] = group_sum<L>(iv[lane]);
+    float part[8], sum[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[k] = (float)(iv[(3 * lane + k) & 63] + k);
+    wave_fsum8(part, sum);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[(9 + k) * 64 + lane] = __float_as_int(sum[k]);
 }
 
 // ---- host-side launch dispatch ------------------------------------------------------------
@@ -1540,7 +1554,7 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 8) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 10) ==
                    hipSuccess ? 0 : -1;
 }
 #endif

@@ -664,6 +664,44 @@ __device__ __forceinline__ float wave_fsum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Eight sums over the wavefront's 64 lanes at once, each returned uniform: a transposed
+// butterfly whose levels halve the values a lane carries -- lane ^ 32 and lane ^ 16 by the gfx950
+// permlane swaps (no selects: the swap pairs two values' halves), lane ^ 1 by DPP quad_perm --
+// and then row rotations by 2, 4 and 8 add the eight lanes of a row that carry the same sum.
+// Every sum is a six-level tree like wave_fsum's, in ~26 instructions for all eight instead of
+// ~14 dependent ones each. Sum s ends on lane (s & 1) + 16 ((s >> 1) & 1) + 32 (s >> 2).
+__device__ __forceinline__ void wave_fsum8(const float (&v)[8], float (&s)[8]) {
+    float a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // lanes 0-31: sum k; lanes 32-63: sum k + 4
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]),
+                                                        __float_as_uint(v[k + 4]), false, false);
+        a[k] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+    float b[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // rows 0..3: sums k, k + 2, k + 4, k + 6
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[k]),
+                                                        __float_as_uint(a[k + 2]), false, false);
+        b[k] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+    const bool odd = (__lane_id() & 1) != 0;  // even lanes keep b[0], odd lanes b[1]
+    const float keep = odd ? b[1] : b[0], send = odd ? b[0] : b[1];
+    float d = keep + __int_as_float(dpp_mov<0xB1>(__float_as_int(send)));  // quad_perm [1,0,3,2]
+    d += __int_as_float(dpp_mov<0x122>(__float_as_int(d)));                // row_ror:2
+    d += __int_as_float(dpp_mov<0x124>(__float_as_int(d)));                // row_ror:4
+    d += __int_as_float(dpp_mov<0x128>(__float_as_int(d)));                // row_ror:8
+    const int di = __float_as_int(d);
+    s[0] = __int_as_float(__builtin_amdgcn_readlane(di, 0));
+    s[1] = __int_as_float(__builtin_amdgcn_readlane(di, 1));
+    s[2] = __int_as_float(__builtin_amdgcn_readlane(di, 16));
+    s[3] = __int_as_float(__builtin_amdgcn_readlane(di, 17));
+    s[4] = __int_as_float(__builtin_amdgcn_readlane(di, 32));
+    s[5] = __int_as_float(__builtin_amdgcn_readlane(di, 33));
+    s[6] = __int_as_float(__builtin_amdgcn_readlane(di, 48));
+    s[7] = __int_as_float(__builtin_amdgcn_readlane(di, 49));
+}
+
 // Whether Accept certainly rejects this proposal, for a chain that owns the wavefront. n
 // objects, c clearances, nrel relationships, ncl non-zero Clearance terms. The arithmetic after
 // the lane sums is fp32 on wave-uniform values; every intermediate has at most ~30 roundings
@@ -680,16 +718,15 @@ __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, 
                        (2.0f * ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
                        (8.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
                        12.0f * U * (afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
-    const float s_nx = wave_fsum(bt.nx), s_ny = wave_fsum(bt.ny);
-    const float s_pw = wave_fsum(bt.pw), s_ang = wave_fsum(bt.ang);
-    const float s_lin = wave_fsum(lin), s_elin = wave_fsum(elin);
-    // sums of |t|: equal to |sum| when no lane holds a term of the other sign (the usual case)
-    float a_nx = fabsf(s_nx), a_ny = fabsf(s_ny), a_ang = fabsf(s_ang);
-    if (__ballot(bt.anx != bt.nx || bt.any != bt.ny || bt.aang != -bt.ang) != 0) {
-        a_nx = wave_fsum(bt.anx);
-        a_ny = wave_fsum(bt.any);
-        a_ang = wave_fsum(bt.aang);
-    }
+    // sums of |t| for VisualBalance: one sum of |area x| + |area y| bounds both coordinates'
+    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin, bt.anx + bt.any, bt.aang};
+    float sum[8];
+    wave_fsum8(part, sum);
+    const float s_nx = sum[0], s_ny = sum[1], s_pw = sum[2], s_ang = sum[3], s_lin = sum[4],
+                s_elin = sum[5];
+    // (each partial of anx + any is rounded once more: 1.25 e below absorbs it)
+    const float a_nx = fmaxf(fabsf(s_nx), sum[6]), a_ny = fmaxf(fabsf(s_ny), sum[6]),
+                a_ang = fmaxf(fabsf(s_ang), sum[7]);
     // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
     const float id = fabsf(rm.inv_denom);
     const float cv = (2.0f * n + 26.0f + kf) * U;

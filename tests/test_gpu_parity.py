@@ -340,6 +340,11 @@ def test_group_collectives(mh, hiplib, L):
             assert np.array_equal(got["scan"][sl], np.concatenate([[0], np.cumsum(ig)[:-1]]))
             assert np.all(got["total"][sl] == ig.sum())
             assert np.all(got["imax"][sl] == ig.max()) and np.all(got["isum"][sl] == ig.sum())
+        # wave_fsum8 (the rejection bound's eight wavefront sums, mh_common.h): exact integer
+        # sums, the same value on every lane
+        for k in range(8):
+            want = sum(int(iv[(3 * lane + k) & 63]) + k for lane in range(64))
+            assert np.all(got["wsum8"][k] == np.float32(want)), (k, got["wsum8"][k], want)
 
 
 @pytest.mark.parametrize("step", STEPS)

@@ -43,6 +43,10 @@ def main():
     print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes} delta={delta}")
     for name, v in zip(names, out[:8]):
         print(f"  {name:18s} {100.0 * v / tot:6.2f}%   {v / per:10.1f} {unit}")
+    if not delta and out[8]:
+        steps = chains * iters
+        print(f"  rejection bound evaluated on {out[8] / steps:.4f} of steps, certain reject on "
+              f"{out[9] / steps:.4f} ({out[9] / out[8]:.4f} of those evaluated)")
     if delta:
         steps = chains * iters
         print(f"  mean Clearance list {out[8] / steps:.2f}, SurfaceArea list {out[9] / steps:.2f}, "
