@@ -173,6 +173,7 @@ def main() -> int:
     offset, count = shard(rank, args.chains)
     sess = mh.Session(room, count, seed=args.seed, device=device, chain_offset=offset)
     lanes, cpw, step_kernel = sess.step_kernel()
+    resident = sess.occupancy()
 
     for _ in range(args.warmup):
         sess.run(args.iters, handle)
@@ -254,6 +255,7 @@ def main() -> int:
                 "mh_steps_per_step": args.iters,
                 "mh_steps_total": (args.warmup + args.steps) * args.iters,
                 "lanes_per_chain": lanes, "chains_per_workgroup": cpw,
+                "resident_chains_per_cu": resident,
                 "step_kernel": step_kernel,
                 "parallelism": f"chain-sharded x{world} (RCCL best-cost all-gather)",
             },

@@ -267,6 +267,10 @@ MH_API int mh_session_summary(mh_session* s, mh_summary* out);
 MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain,
                                int* chains_per_workgroup, int* incremental);
 
+/* Chains of this session's step kernel that one CU keeps resident, as the runtime's occupancy
+ * calculator counts them (registers, LDS and the wave limit of its launch shape). */
+MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu);
+
 MH_API void mh_session_destroy(mh_session* s);
 
 /* ---- diagnostics -------------------------------------------------------------------------- */

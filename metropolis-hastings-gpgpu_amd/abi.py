@@ -123,7 +123,8 @@ COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointC
 EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelWrapperEx", "KernelFreeResult",
            "KernelLastError", "KernelEvaluateCosts", "mh_session_create", "mh_session_create_ex",
            "mh_session_run", "mh_session_finalize",
-           "mh_session_download", "mh_session_current_costs", "mh_session_summary", "mh_session_geometry",
+           "mh_session_download", "mh_session_current_costs", "mh_session_summary",
+           "mh_session_geometry", "mh_session_occupancy",
            "mh_session_destroy", "mh_debug_rng", "mh_debug_rng_ex", "mh_debug_collectives"]
 
 P = C.POINTER
@@ -178,6 +179,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_session_summary.restype = C.c_int
     lib.mh_session_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
     lib.mh_session_geometry.restype = C.c_int
+    lib.mh_session_occupancy.argtypes = [C.c_void_p, P(C.c_int)]
+    lib.mh_session_occupancy.restype = C.c_int
     lib.mh_session_destroy.argtypes = [C.c_void_p]
     lib.mh_session_destroy.restype = None
     lib.mh_debug_collectives.argtypes = [C.c_int, P(C.c_float), P(C.c_int), P(C.c_int)]
@@ -378,6 +381,13 @@ class Session:
         lanes, cpw, inc = C.c_int(), C.c_int(), C.c_int()
         self.lib.mh_session_geometry(self.h, C.byref(lanes), C.byref(cpw), C.byref(inc))
         return lanes.value, cpw.value, "incremental" if inc.value else "full"
+
+    def occupancy(self) -> int:
+        """Chains of the step kernel one CU keeps resident (the runtime's occupancy count)."""
+        c = C.c_int()
+        if self.lib.mh_session_occupancy(self.h, C.byref(c)) != 0:
+            raise MHError(last_error(self.lib))
+        return c.value
 
     def close(self):
         if getattr(self, "h", None):

@@ -867,6 +867,22 @@ MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* c
     return 0;
 }
 
+MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
+    if (!s || !chains_per_cu) { set_error("NULL argument"); return -1; }
+    const auto& g = s->geo;
+    int blocks = 0;
+    if (g.delta) {
+        blocks = mh::delta_blocks_per_cu(g.dL, g.dwaves,
+                                         mh::delta_lds_bytes(s->geo.dlay, g.dL, g.dwaves));
+        *chains_per_cu = blocks * g.dwaves * (64 / g.dL);
+    } else {
+        blocks = mh::step_blocks_per_cu(g.L, g.npl, g.waves,
+                                        mh::lds_bytes(s->geo.lay, g.L, g.waves));
+        *chains_per_cu = blocks * g.waves * (64 / g.L);
+    }
+    return 0;
+}
+
 MH_API void mh_session_destroy(mh_session* s) { free_session(s); }
 
 // Diagnostic: the Philox words, uniforms and normals a chain with this (seed, subsequence)

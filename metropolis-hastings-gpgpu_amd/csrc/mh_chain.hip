@@ -67,19 +67,51 @@ struct ChainAux {
 };
 static_assert(sizeof(ChainAux) <= kChainAuxBytes, "ChainAux");
 
+// The double pose (x, y, rotY) of the objects this lane owns, m * L + r for m < NPL, kept in
+// registers for the whole launch: every cost term reads a lane's own objects, and the few
+// reads of another object's pose (the proposal's objects, a symmetry row's leader column) go
+// lane to lane. LDS keeps only the float pose words (ObjP) that the O(N^2) scans read.
+template <int NPL>
+struct OwnPose {
+    double x[NPL], y[NPL], ry[NPL];
+};
+
+// rotY of object j, group-uniform j: from its owner lane (readlane / ds_bpermute).
+template <int L, int NPL>
+__device__ __forceinline__ double pose_ry(const OwnPose<NPL>& op, int j, int gbase) {
+    return grp_get<L>(sel<NPL>(op.ry, j / L), j % L, gbase);
+}
+
+// rotY of object j where j differs between lanes (j < 0 reads object 0): one ds_bpermute per
+// owned slot, then the slot's value. Call with every lane of the wavefront active.
+template <int L, int NPL>
+__device__ __forceinline__ double pose_ry_var(const OwnPose<NPL>& op, int j, int gbase) {
+    const int jj = j < 0 ? 0 : j;
+    const int addr = (gbase + jj % L) << 2;
+    const int slot = jj / L;
+    double out = 0.0;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int2 w = *reinterpret_cast<const int2*>(&op.ry[m]);
+        int2 o;
+        o.x = __builtin_amdgcn_ds_bpermute(addr, w.x);
+        o.y = __builtin_amdgcn_ds_bpermute(addr, w.y);
+        out = (m == slot) ? *reinterpret_cast<double*>(&o) : out;
+    }
+    return out;
+}
+
 struct ChainPtrs {
     const RectShape* objs;  // room tables, staged once per workgroup into LDS (ChainLds)
     const RectShape* clrs;
     const RelConst* relc;
     ObjP* P;
-    double* RY;
     double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
     double *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
     double* LCL;      // compacted non-zero Clearance terms (float values), capacity 2L
     double* LPW;      // compacted non-zero PairWise / Angle terms, capacity lst_r each
     double* LANG;
     int lst_r;
-    double *X, *Y;
     double* zrr;      // HBM: this chain's z, rotX, rotZ rows (F_Z, F_RX, F_RZ of the pose block)
     float4* OFF;
     float4* CLA;
@@ -214,7 +246,8 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
 // the bound already decides Accept's rejection for the drawn uniform `u_acc`, the function
 // returns with *fast_reject set and `out` unset; otherwise it goes on to the exact costs.
 template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false>
-__device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int gbase,
+__device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPose<NPL>& op,
+                           int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
                            float cur_total = 0.0f, bool* fast_reject = nullptr) {
@@ -242,45 +275,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         const int i = m * L + r;
         px[m] = py[m] = 0.0;
         cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
-        sao[m] = sac[m] = boxo[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i < n) {
-            const RectShape os = ch.objs[i];
-            const float area = __int_as_float(os.pad);
-            const ObjP p = ch.P[i];
-            const double x = ch.X[i], y = ch.Y[i];
-            wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(ch.RY[i]) < 1e15);
-            // VisualBalanceCosts products, Kernel.cu:200-201.
-            px[m] = (double)area * x;
-            py[m] = (double)area * y;
-            // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
-            // object per lane: below, sharing the relationship terms' atan2 pass).
-            if (!(MH_ABLATE & 2) && !SHARED) {
-                float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
-                float b = at - p.rotYf;
-                float ph = (float)((double)b + kHalfPI);
-                cph[m] = cos_f32(ph);
-            }
-            // SymmetryCosts row setup, Kernel.cu:292-299.
-            double al = x * (double)rm.ux;
-            al = al + y * (double)rm.uy;
-            float sd = (float)(2.0 * (rm.along_f - al));
-            rxs[m] = (float)(x + (double)(sd * rm.ux));
-            rys[m] = (float)(y + (double)(sd * rm.uy));
-            float rr = (float)(rm.two_focal_rot - ch.RY[i]);
-            if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
-            rrs[m] = rr;
-            // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
-            const float4 box = shape_box(os, p.xf, p.yf);
-            if constexpr (WITH_OL) ch.OFF[i] = box;
-            sao[m] = comp_overlaps(rm, box);
-            boxo[m] = box;
-        }
         rpw[m] = rang[m] = 0.0;
+        sao[m] = sac[m] = boxo[m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (SHARED) {
             // Steps, one object per lane: only the moved objects' FocalPoint terms and the
             // relationships they touch change; the rest keep their terms. Both need an atan2
             // (phi, Kernel.cu:187; theta, :175): one shared pass serves a lane's relationship
             // or, failing that, its object; a lane that needs both takes a second (rare) pass.
+            // (It runs first, so the per-object values below are not live across the atan2.)
             const bool obj = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
             bool rel = false;
             if (i < rm.r && !(MH_ABLATE & 16)) {
@@ -311,8 +313,41 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 rpw[m] = clp.rpw;
                 rang[m] = clp.rang;
             }
-        } else if (!(MH_ABLATE & 16) && i < rm.r) {
-            rel_terms(ch, i, rpw[m], rang[m]);
+        }
+        if (i < n) {
+            const RectShape os = ch.objs[i];
+            const float area = __int_as_float(os.pad);
+            const ObjP p = ch.P[i];
+            const double x = op.x[m], y = op.y[m];
+            wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(op.ry[m]) < 1e15);
+            // VisualBalanceCosts products, Kernel.cu:200-201.
+            px[m] = (double)area * x;
+            py[m] = (double)area * y;
+            // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
+            // object per lane: above, sharing the relationship terms' atan2 pass).
+            if (!(MH_ABLATE & 2) && !SHARED) {
+                float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
+                float b = at - p.rotYf;
+                float ph = (float)((double)b + kHalfPI);
+                cph[m] = cos_f32(ph);
+            }
+            // SymmetryCosts row setup, Kernel.cu:292-299.
+            double al = x * (double)rm.ux;
+            al = al + y * (double)rm.uy;
+            float sd = (float)(2.0 * (rm.along_f - al));
+            rxs[m] = (float)(x + (double)(sd * rm.ux));
+            rys[m] = (float)(y + (double)(sd * rm.uy));
+            float rr = (float)(rm.two_focal_rot - op.ry[m]);
+            if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
+            rrs[m] = rr;
+            // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
+            const float4 box = shape_box(os, p.xf, p.yf);
+            if constexpr (WITH_OL) ch.OFF[i] = box;
+            sao[m] = comp_overlaps(rm, box);
+            boxo[m] = box;
+        }
+        if constexpr (!SHARED) {
+            if (!(MH_ABLATE & 16) && i < rm.r) rel_terms(ch, i, rpw[m], rang[m]);
         }
         if constexpr (NPL == 1) {
             clo.rpw = rpw[0];
@@ -386,9 +421,10 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         amb[m] = row && (exact_mode || !clear);
         any_amb |= amb[m];
         float e = 0.0f;
+        const double ry1 = pose_ry_var<L, NPL>(op, j1[m], gbase);  // (every lane active)
         if (row && j1[m] >= 0) {
             const ObjP q = ch.P[j1[m]];
-            e = sym_val_exact(q.xf, q.yf, ch.RY[j1[m]], rxs[m], rys[m], (double)rrs[m]);
+            e = sym_val_exact(q.xf, q.yf, ry1, rxs[m], rys[m], (double)rrs[m]);
         }
         sym.mx[m] = fmaxf(0.0f, e);
         sym.arg[m] = e > 0.0f ? j1[m] : -1;
@@ -406,13 +442,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         }
         for (int j = 0; j < n; ++j) {
             const ObjP q = ch.P[j];
+            const double ryj = pose_ry<L, NPL>(op, j, gbase);
 #pragma unroll
             for (int m = 0; m < NPL; ++m) {
                 if (amb[m]) {
                     const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rxs[m],
                                                  rys[m], rrs[m]);
                     if (!(v < m1[m] - thr[m])) {
-                        const float e = sym_val_exact(q.xf, q.yf, ch.RY[j], rxs[m], rys[m],
+                        const float e = sym_val_exact(q.xf, q.yf, ryj, rxs[m], rys[m],
                                                       (double)rrs[m]);
                         if (e > sym.mx[m]) {
                             sym.mx[m] = e;
@@ -435,6 +472,9 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
     float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
     if (ka >= 0) qa = *reinterpret_cast<const float4*>(&ch.P[ka]);
     if (kb >= 0) qb = *reinterpret_cast<const float4*>(&ch.P[kb]);
+    // the changed columns' rotY, from their owner lanes (ka, kb are group-uniform)
+    const double rya = pose_ry<L, NPL>(op, ka < 0 ? 0 : ka, gbase);
+    const double ryb = pose_ry<L, NPL>(op, kb < 0 ? 0 : kb, gbase);
     bool any_pend = false;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
@@ -476,7 +516,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
             const unsigned pm = sel<NPL>(pend, ms);
             const int col = (pm & 1u) ? ka : kb;
             const ObjP q = ch.P[col];
-            const float e = sym_val_exact(q.xf, q.yf, ch.RY[col], sel<NPL>(rxs, ms),
+            const float e = sym_val_exact(q.xf, q.yf, (pm & 1u) ? rya : ryb, sel<NPL>(rxs, ms),
                                           sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
             any_pend = false;
 #pragma unroll
@@ -540,11 +580,14 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
                 (exact_mode || ld.j < 0) ? INFINITY : 2.0f * sym_err(fabsf(ld.m) + 1.0f, rr);
             float bv = -INFINITY;
             int bj = -1;
-            for (int j = r; j < n; j += L) {
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) {  // this lane's columns j = q * L + r
+                const int j = q * L + r;
+                if (j >= n) break;
                 const ObjP p = ch.P[j];
                 const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
                 if (!(v < ld.m - thr)) {
-                    const float e = sym_val_exact(p.xf, p.yf, ch.RY[j], rx, ry, (double)rr);
+                    const float e = sym_val_exact(p.xf, p.yf, op.ry[q], rx, ry, (double)rr);
                     if (e > bv) {
                         bv = e;
                         bj = j;
@@ -574,12 +617,13 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
         }
     }
     while (__ballot(leadp != 0u)) {
+        const int ms = leadp ? __builtin_ctz(leadp) : 0;
+        const int j = leadp ? sel<NPL>(lead, ms) : 0;
+        const double ryj = pose_ry_var<L, NPL>(op, j, gbase);  // (every lane active)
         if (leadp) {
-            const int ms = __builtin_ctz(leadp);
             leadp &= leadp - 1u;
-            const int j = sel<NPL>(lead, ms);
             const ObjP q = ch.P[j];
-            const float e = sym_val_exact(q.xf, q.yf, ch.RY[j], sel<NPL>(rxs, ms),
+            const float e = sym_val_exact(q.xf, q.yf, ryj, sel<NPL>(rxs, ms),
                                           sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
 #pragma unroll
             for (int m = 0; m < NPL; ++m) {
@@ -895,33 +939,48 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, int r, int 
 
 // ---- propose(), Kernel.cu:566-704, applied in place --------------------------------------
 
-__device__ __forceinline__ Backup read_obj(const ChainPtrs& ch, int k) {
+// Object k's pose (k group-uniform), from its owner lane.
+template <int L, int NPL>
+__device__ __forceinline__ Backup read_obj(const OwnPose<NPL>& op, int k, int gbase) {
     Backup b;
     b.k = k;
-    b.x = ch.X[k];
-    b.y = ch.Y[k];
-    b.ry = ch.RY[k];
+    const int m = k / L, src = k % L;
+    b.x = grp_get<L>(sel<NPL>(op.x, m), src, gbase);
+    b.y = grp_get<L>(sel<NPL>(op.y, m), src, gbase);
+    b.ry = grp_get<L>(sel<NPL>(op.ry, m), src, gbase);
     return b;
 }
 
-__device__ __forceinline__ void write_obj(const ChainPtrs& ch, int k, double x, double y,
-                                          double ry) {
-    ch.X[k] = x;
-    ch.Y[k] = y;
-    ObjP p;
-    p.xf = (float)x;
-    p.yf = (float)y;
-    p.rotYf = (float)ry;
-    p.pad = 0.0f;
-    ch.P[k] = p;
-    ch.RY[k] = ry;
+// Sets object k's pose (group-uniform k and values): its owner lane's registers, and the float
+// pose words in LDS (`writer`).
+template <int L, int NPL>
+__device__ __forceinline__ void write_obj(const ChainPtrs& ch, OwnPose<NPL>& op, int r,
+                                          bool writer, int k, double x, double y, double ry) {
+    const bool own = r == k % L;
+    const int km = k / L;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const bool here = own && m == km;
+        op.x[m] = here ? x : op.x[m];
+        op.y[m] = here ? y : op.y[m];
+        op.ry[m] = here ? ry : op.ry[m];
+    }
+    if (writer) {
+        ObjP p;
+        p.xf = (float)x;
+        p.yf = (float)y;
+        p.rotYf = (float)ry;
+        p.pad = 0.0f;
+        ch.P[k] = p;
+    }
 }
 
-// Applies one proposal to the configuration in LDS; `writer` also records the overwritten
-// objects in ch.aux so a rejection can undo them. Returns the objects it changed (-1: none).
-template <class Rng>
+// Applies one proposal to the configuration (registers and LDS); `writer` also records the
+// overwritten objects in ch.aux so a rejection can undo them. Returns the objects it changed
+// (-1: none).
+template <int L, int NPL, class Rng>
 __device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen,
-                        const ChainPtrs& ch, bool writer) {
+                        const ChainPtrs& ch, OwnPose<NPL>& op, int r, int gbase, bool writer) {
     const int n = rm.n;
     const int mode = rand_int(rng, 2, 0);
     if (mode == 0) {  // translate, Kernel.cu:595-632
@@ -930,7 +989,7 @@ __device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen
         dx = dx * rm.sx;
         float dy = rng.normal();
         dy = dy * rm.sy;
-        const Backup b0 = read_obj(ch, k);
+        const Backup b0 = read_obj<L, NPL>(op, k, gbase);
         double x = b0.x, y = b0.y;
         if (x + (double)dx > rm.rmax_x) x = rm.rmax_x;
         else if (x + (double)dx < rm.rmin_x) x = rm.rmin_x;
@@ -942,15 +1001,15 @@ __device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen
             ch.aux->b[0] = b0;
             ch.aux->nb = 1;
             ch.aux->swap_a = -1;
-            write_obj(ch, k, x, y, b0.ry);
         }
+        write_obj<L, NPL>(ch, op, r, writer, k, x, y, b0.ry);
         return make_int2(k, -1);
     }
     if (mode == 1) {  // rotate, Kernel.cu:634-653
         const int k = pick_object(rng, n, frozen);
         float dr = rng.normal();
         dr = (float)((double)dr * kSigmaT);
-        const Backup b0 = read_obj(ch, k);
+        const Backup b0 = read_obj<L, NPL>(op, k, gbase);
         double ry = b0.ry + (double)dr;
         if (ry < 0) ry = ry + kTwoPI;
         else if (ry > kTwoPI) ry = ry - kTwoPI;
@@ -958,8 +1017,8 @@ __device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen
             ch.aux->b[0] = b0;
             ch.aux->nb = 1;
             ch.aux->swap_a = -1;
-            write_obj(ch, k, b0.x, b0.y, ry);
         }
+        write_obj<L, NPL>(ch, op, r, writer, k, b0.x, b0.y, ry);
         return make_int2(k, -1);
     }
     // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
@@ -972,18 +1031,51 @@ __device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen
     }
     const int ka = pick_object(rng, n, frozen);
     const int kb = pick_object(rng, n, frozen);
+    const Backup b0 = read_obj<L, NPL>(op, ka, gbase);
+    const Backup b1 = read_obj<L, NPL>(op, kb, gbase);
     if (writer) {
-        const Backup b0 = read_obj(ch, ka);
-        const Backup b1 = read_obj(ch, kb);
         ch.aux->b[0] = b0;
         ch.aux->b[1] = b1;
         ch.aux->nb = 2;
         ch.aux->swap_a = ka;
         ch.aux->swap_b = kb;
-        write_obj(ch, ka, b1.x, b1.y, b1.ry);
-        write_obj(ch, kb, (double)(float)b0.x, (double)(float)b0.y, (double)(float)b0.ry);
     }
+    write_obj<L, NPL>(ch, op, r, writer, ka, b1.x, b1.y, b1.ry);
+    write_obj<L, NPL>(ch, op, r, writer, kb, (double)(float)b0.x, (double)(float)b0.y,
+                      (double)(float)b0.ry);
     return make_int2(ka, kb == ka ? -1 : kb);
+}
+
+// Saves the proposed configuration as the chain's best (cfgStar, Kernel.cu:810-811): lane r
+// writes its objects' x, y, rotY from registers; z, rotX, rotZ come from HBM with a pending swap
+// applied as commit_swap_zrr would (ka takes kb's values, kb takes ka's rounded to float).
+template <int L, int NPL>
+__device__ __forceinline__ void save_best_pose(const ChainPtrs& ch, const OwnPose<NPL>& op,
+                                               double* dst, int n, int r) {
+    const int ka = ch.aux->swap_a, kb = ch.aux->swap_b;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        if (i >= n) break;
+        dst[F_X * n + i] = op.x[m];
+        dst[F_Y * n + i] = op.y[m];
+        dst[F_RY * n + i] = op.ry[m];
+        int src = i;
+        bool rnd = false;
+        if (ka >= 0) {
+            if (i == kb) {
+                src = ka;
+                rnd = true;
+            } else if (i == ka) {
+                src = kb;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const double v = ch.zrr[f * n + src];
+            dst[(F_Z + f) * n + i] = rnd ? (double)(float)v : v;
+        }
+    }
 }
 
 // An accepted swap also exchanges z, rotX and rotZ (Kernel.cu:675-700), which no cost reads:
@@ -1000,22 +1092,33 @@ __device__ __forceinline__ void commit_swap_zrr(const ChainPtrs& ch, int n) {
     }
 }
 
-// Undo the last proposal (writer lane only).
-__device__ __forceinline__ void restore(const ChainPtrs& ch) {
+// Undo the last proposal (every lane of the group; the backups are group-uniform LDS reads).
+template <int L, int NPL>
+__device__ __forceinline__ void restore(const ChainPtrs& ch, OwnPose<NPL>& op, int r,
+                                        bool writer) {
     const int nb = ch.aux->nb;
     for (int q = nb - 1; q >= 0; --q) {
         const Backup b = ch.aux->b[q];
-        write_obj(ch, b.k, b.x, b.y, b.ry);
+        write_obj<L, NPL>(ch, op, r, writer, b.k, b.x, b.y, b.ry);
     }
 }
 
 // ---- the kernel ---------------------------------------------------------------------------
 
-#ifdef MH_WAVES_PER_EU  // occupancy experiments: ask the register allocator for more waves
-#define MH_OCC __attribute__((amdgpu_waves_per_eu(MH_WAVES_PER_EU, 8)))
+// Waves per SIMD the register allocator must leave room for. The plain step kernel with one
+// chain per wavefront and one object per lane (config 3) is held to 5: its LDS then admits five
+// 4-wave workgroups per CU, and 20 resident chains measured 4.47e8 chain-steps/s against 4.20e8
+// with 16 (101 VGPRs). Other instances keep the allocator's choice. $MH_WAVES_PER_EU builds
+// (tools/build_ablate.sh wpeK) pin every instance for experiments.
+template <int L, int NPL, int OP>
+struct StepWaves {
+#ifdef MH_WAVES_PER_EU
+    static constexpr int value = MH_WAVES_PER_EU;
 #else
-#define MH_OCC
+    static constexpr int value = (L == 64 && NPL == 1 && OP == OP_STEP) ? 5 : 1;
 #endif
+};
+#define MH_OCC __attribute__((amdgpu_waves_per_eu(StepWaves<L, NPL, OP>::value, 8)))
 
 // Output slot of a chain: with parallel tempering the replica at rung k of group g goes to
 // g*K + k (a session's chain offset and count are multiples of K).
@@ -1073,7 +1176,6 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.clrs = clrs_l;
     ch.relc = relc_l;
     ch.P = reinterpret_cast<ObjP*>(base + F.P);
-    ch.RY = reinterpret_cast<double*>(base + F.RY);
     ch.PX = reinterpret_cast<double*>(base + F.PX);
     ch.PY = reinterpret_cast<double*>(base + F.PY);
     ch.CPHF = reinterpret_cast<double*>(base + F.CPHF);
@@ -1082,8 +1184,6 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
     ch.lst_r = a.lay.lst_r;
     ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
-    ch.X = reinterpret_cast<double*>(base + F.X);
-    ch.Y = reinterpret_cast<double*>(base + F.Y);
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
     ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
     ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
@@ -1100,28 +1200,35 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         ch.CPHF[i] = 0.0;
         ch.RMXF[i] = 0.0;
     }
-    // Stage the configuration into LDS.
+    // Stage the configuration: double poses into this lane's registers, float pose words
+    // into LDS.
     const double* src;
     if constexpr (OP == OP_INIT) src = a.cfg;
     else if constexpr (OP == OP_EVAL) src = a.cfg + chain * (int64_t)(F_COUNT * n);
     else src = a.st + chain * (int64_t)(F_COUNT * n);
-    for (int i = r; i < n; i += L) {
-        const double x = src[F_X * n + i], y = src[F_Y * n + i];
-        ch.X[i] = x;
-        ch.Y[i] = y;
-        if constexpr (OP == OP_INIT) {  // z, rotX, rotZ live in HBM only
-            ch.zrr[i] = src[F_Z * n + i];
-            ch.zrr[n + i] = src[F_RX * n + i];
-            ch.zrr[2 * n + i] = src[F_RZ * n + i];
+    OwnPose<NPL> op;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+        const int i = m * L + r;
+        op.x[m] = op.y[m] = op.ry[m] = 0.0;
+        if (i < n) {
+            const double x = src[F_X * n + i], y = src[F_Y * n + i];
+            const double ry = src[F_RY * n + i];
+            op.x[m] = x;
+            op.y[m] = y;
+            op.ry[m] = ry;
+            if constexpr (OP == OP_INIT) {  // z, rotX, rotZ live in HBM only
+                ch.zrr[i] = src[F_Z * n + i];
+                ch.zrr[n + i] = src[F_RX * n + i];
+                ch.zrr[2 * n + i] = src[F_RZ * n + i];
+            }
+            ObjP p;
+            p.xf = (float)x;
+            p.yf = (float)y;
+            p.rotYf = (float)ry;
+            p.pad = 0.0f;
+            ch.P[i] = p;
         }
-        ObjP p;
-        p.xf = (float)x;
-        p.yf = (float)y;
-        const double ry = src[F_RY * n + i];
-        p.rotYf = (float)ry;
-        p.pad = 0.0f;
-        ch.P[i] = p;
-        ch.RY[i] = ry;
     }
     wave_sync();
 
@@ -1129,7 +1236,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     SymRows<NPL> sym;  // symmetry row maxima of the current configuration
     if constexpr (OP == OP_INIT) {
         ClPairs cl0;
-        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, cl0, cl0);
+        eval_costs<L, NPL, false, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, cl0, cl0);
         if (r == 0) {
             ChainMeta m;
             m.draws = 0;
@@ -1155,7 +1262,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         if constexpr (TRACK)  // (the extended families also carry parallel tempering)
             if (a.n_temps > 1) beta = a.ladder[m0.rung];
         ClPairs cl;  // non-zero Clearance pairs of the current configuration
-        eval_costs<L, NPL, false, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, cl, cl);
+        eval_costs<L, NPL, false, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, cl, cl);
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 10; ++k) ch.aux->cyc[k] = 0;
@@ -1165,7 +1272,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             unsigned long long ts = 0;
             MH_STAMP(ts);
             rng_prepare(rng);
-            const int2 kk = propose(rng, *rm_l, frozen, ch, writer);
+            const int2 kk = propose<L, NPL>(rng, *rm_l, frozen, ch, op, r, gbase, writer);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
@@ -1178,14 +1285,14 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             bool fast_rej = false;
             float u_acc = 0.0f;
             if constexpr (FASTK) u_acc = rng.uniform();
-            eval_costs<L, NPL, false, true, FASTK>(a, ch, r, gbase, sc, ss, sym, kk.x, kk.y, cls,
-                                                    cl, u_acc, cur_total, &fast_rej);
+            eval_costs<L, NPL, false, true, FASTK>(a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y,
+                                                    cls, cl, u_acc, cur_total, &fast_rej);
             MH_STAMP(ts);
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if constexpr (TRACK) {
                 if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
                     best_total = sc[0];
-                    save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
+                    save_best_pose<L, NPL>(ch, op, a.best + chain * (int64_t)(F_COUNT * n), n, r);
                 }
             }
             bool acc;
@@ -1203,8 +1310,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
                     commit_swap_zrr(ch, n);
                 }
-            } else if (writer) {
-                restore(ch);
+            } else {
+                restore<L, NPL>(ch, op, r, writer);
             }
             wave_sync();
             if (writer) MH_PHASE(ch, 7, ts);
@@ -1227,7 +1334,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
         ClPairs clf;
-        eval_costs<L, NPL, true, false>(a, ch, r, gbase, cur, sym, sym, -1, -1, clf, clf);
+        eval_costs<L, NPL, true, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, clf, clf);
         if (r == 0) {
             resultCosts rc;
             rc.totalCosts = cur[0];
@@ -1241,13 +1348,16 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             a.costs[out_index(a, chain)] = rc;
         }
         if constexpr (OP == OP_FINAL) {
-            for (int i = r; i < n; i += L) {
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) {
+                const int i = m * L + r;
+                if (i >= n) break;
                 point p;
-                p.x = (float)ch.X[i];
-                p.y = (float)ch.Y[i];
+                p.x = (float)op.x[m];
+                p.y = (float)op.y[m];
                 p.z = (float)ch.zrr[i];
                 p.rotX = (float)ch.zrr[n + i];
-                p.rotY = (float)ch.RY[i];
+                p.rotY = (float)op.ry[m];
                 p.rotZ = (float)ch.zrr[2 * n + i];
                 a.pts[out_index(a, chain) * (int64_t)n + i] = p;
             }
@@ -1256,17 +1366,20 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 
     if constexpr (OP == OP_INIT || STEP) {
         double* dst = a.st + chain * (int64_t)(F_COUNT * n);
-        for (int i = r; i < n; i += L) {
-            dst[F_X * n + i] = ch.X[i];
-            dst[F_Y * n + i] = ch.Y[i];
-            dst[F_RY * n + i] = ch.RY[i];
+#pragma unroll
+        for (int m = 0; m < NPL; ++m) {
+            const int i = m * L + r;
+            if (i >= n) break;
+            dst[F_X * n + i] = op.x[m];
+            dst[F_Y * n + i] = op.y[m];
+            dst[F_RY * n + i] = op.ry[m];
         }
     }
     if constexpr (OP == OP_INIT) {
         if (a.track != TRACK_OFF) {  // cfgBest := cfgCurrent, Kernel.cu:779-782
             if (r == 0) ch.aux->swap_a = -1;
             wave_sync();
-            save_best(ch, a.best + chain * (int64_t)(F_COUNT * n), n, r, L);
+            save_best_pose<L, NPL>(ch, op, a.best + chain * (int64_t)(F_COUNT * n), n, r);
         }
     }
 }
@@ -1510,6 +1623,29 @@ int choose_lanes(int n, int64_t n_chains, int64_t resident_waves) {
 }
 int choose_npl(int n, int L) { return (n + L - 1) / L; }
 int max_npl() { return 8; }
+
+// Resident workgroups per CU of the plain step kernel for a launch shape (registers, LDS and
+// the wave limit, as the runtime counts them). 0 if it does not fit.
+template <int L>
+static int step_blocks_l(int npl, int threads, size_t lds) {
+    int blocks = 0;
+    hipError_t e;
+    if (npl <= 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 1, OP_STEP>, threads, lds);
+    else if (npl <= 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 2, OP_STEP>, threads, lds);
+    else if (npl <= 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 4, OP_STEP>, threads, lds);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 8, OP_STEP>, threads, lds);
+    return e == hipSuccess ? blocks : 0;
+}
+
+int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds) {
+    const int threads = 64 * waves_per_wg;
+    switch (L) {
+        case 8: return step_blocks_l<8>(npl, threads, lds);
+        case 16: return step_blocks_l<16>(npl, threads, lds);
+        case 32: return step_blocks_l<32>(npl, threads, lds);
+        default: return step_blocks_l<64>(npl, threads, lds);
+    }
+}
 
 size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
     return (size_t)lay.hdr + (size_t)waves_per_wg * (64 / L) * lay.stride;

@@ -145,9 +145,8 @@ struct ChainLds {
     int h_rel;   // RelConst[R]
     int h_frz;   // unsigned char[N + 1] frozen flags (index N counts as frozen)
     int h_room;  // DevRoom copy (read by the out-of-line cost evaluation)
-    int P;       // ObjP[N]   {float xf, yf, rotYf, pad}
-    int RY;      // double[N] rotY
-    int X, Y;    // double[N]   (z, rotX, rotZ never enter a cost: they stay in HBM)
+    int P;       // ObjP[N]   {float xf, yf, rotYf, pad} (the double x, y, rotY live in the
+                 // owner lanes' registers; z, rotX, rotZ never enter a cost: they stay in HBM)
     int OFF;     // float4[N] off-limits boxes (final / evaluation passes only; -1 in the step)
     int CLA;     // float4[C] clearance boxes at their source objects
     int NZ;      // uint64[2][C] non-zero Clearance pairs per clearance row (bit j: object j),
@@ -276,7 +275,7 @@ inline MH_HD constexpr int bank_place_c(int o, unsigned& used) {
 // clearance shapes; the relationship table follows at a run-time offset.
 struct FixedLds {
     int h_room, h_obj, h_frz, h_zero, h_clr;            // workgroup header (h_zero: 4 zero doubles)
-    int P, RY, X, Y, AUX, PX, PY, CPHF, RMXF, LCL, end;  // per chain
+    int P, AUX, PX, PY, CPHF, RMXF, LCL, end;  // per chain
 };
 
 inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
@@ -289,9 +288,6 @@ inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
     f.h_clr = f.h_zero + 32;
     int o = 0;
     f.P = o;   o += 16 * NC;
-    f.RY = o;  o += 8 * NC;
-    f.X = o;   o += 8 * NC;
-    f.Y = o;   o += 8 * NC;
     f.AUX = o; o += kChainAuxBytes;
     // The replay's streams, all doubles (float terms are widened when written, one instruction
     // for all lanes, instead of inside the serial walk): lanes 0..4, 6, 7 read PX, PY, CPHF,
@@ -321,9 +317,6 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off 
     l.h_rel = h;  h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
     l.hdr = h;
     l.P = f.P;
-    l.RY = f.RY;
-    l.X = f.X;
-    l.Y = f.Y;
     l.AUX = f.AUX;
     l.PX = f.PX;
     l.PY = f.PY;
