@@ -225,39 +225,33 @@ struct Geometry {
     mh::DeltaLds dlay;
 };
 
-// Incremental step kernel geometry: the (lanes per chain, waves per workgroup) shape that keeps
-// the most chains resident per CU, as the runtime's occupancy calculator counts them (registers,
-// LDS, waves); ties go to more waves, i.e. more lanes per chain (L = 64 holds the kernel at ~96
-// VGPRs; L < 64 needs ~166). It is the default step above N = 128 (measured, chain-steps/s
-// full vs incremental: N = 100 1.21e8 / 1.15e8, N = 128 8.8e7 / 8.8e7, N = 192 2.0e7 / 5.0e7,
-// N = 256 8.9e6 / 3.1e7). $MH_DELTA=0/1 forces the choice; $MH_DELTA_LANES /
-// $MH_DELTA_WAVES pin a shape.
+// Incremental step kernel geometry: one chain per wavefront; the workgroup size (chains per
+// workgroup, up to 12) that keeps the most chains resident per CU, as the runtime's occupancy
+// calculator counts them (registers, LDS, waves); ties go to fewer waves per workgroup. The
+// kernel is latency-bound, so resident chains are its throughput (measured at N = 256: 1 to 5
+// chains per CU gave 6.6e6 to 3.3e7 chain-steps/s, the launch time unchanged). It is the
+// default step above N = 128 (measured, chain-steps/s full vs incremental: N = 100 1.21e8 /
+// 1.15e8, N = 128 8.8e7 / 8.8e7, N = 192 2.0e7 / 5.0e7, N = 256 8.9e6 / 3.1e7). $MH_DELTA=0/1
+// forces the choice; $MH_DELTA_WAVES pins the workgroup size.
 void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     g.dlay = mh::make_delta_layout(n, c, r);
     const char* e = getenv("MH_DELTA");
     g.delta = e && *e ? atoi(e) != 0 : n > 128;
-    const int want_l = getenv("MH_DELTA_LANES") ? atoi(getenv("MH_DELTA_LANES")) : 0;
     const int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
-    int best_chains = -1, best_waves = -1;
-    g.dL = 0;
-    for (int L : {8, 16, 32, 64}) {
-        if (want_l && L != want_l) continue;
-        for (int w = 1; w <= 8; ++w) {
-            if (want_w && w != want_w) continue;
-            const size_t b = mh::delta_lds_bytes(g.dlay, L, w);
-            if (b > (size_t)max_lds) continue;
-            const int blocks = mh::delta_blocks_per_cu(L, w, b);
-            const int waves = blocks * w;
-            const int chains = waves * (64 / L);
-            if (chains > best_chains || (chains == best_chains && waves > best_waves)) {
-                best_chains = chains;
-                best_waves = waves;
-                g.dL = L;
-                g.dwaves = w;
-            }
+    int best_chains = -1;
+    g.dL = 64;
+    g.dwaves = 0;
+    for (int w = 1; w <= 12; ++w) {  // (the kernel's launch bound: 768 threads)
+        if (want_w && w != want_w) continue;
+        const size_t b = mh::delta_lds_bytes(g.dlay, w);
+        if (b > (size_t)max_lds) continue;
+        const int chains = mh::delta_blocks_per_cu(n, w, b) * w;
+        if (chains > best_chains) {
+            best_chains = chains;
+            g.dwaves = w;
         }
     }
-    if (g.dL == 0 || best_chains <= 0) g.delta = false;  // does not fit: full evaluation
+    if (g.dwaves == 0 || best_chains <= 0) g.delta = false;  // does not fit: full evaluation
 }
 
 bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, Geometry& g) {
@@ -498,7 +492,7 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
         if (s->n_temps > 1)  // stop at the next exchange round
             chunk = (int)std::min<int64_t>(chunk, s->swap_interval - s->steps_done % s->swap_interval);
         a.iterations = chunk;
-        if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dL, s->geo.dwaves, st));
+        if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dwaves, st));
         else MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
         done += chunk;
         s->steps_done += chunk;
@@ -872,9 +866,9 @@ MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
     const auto& g = s->geo;
     int blocks = 0;
     if (g.delta) {
-        blocks = mh::delta_blocks_per_cu(g.dL, g.dwaves,
-                                         mh::delta_lds_bytes(s->geo.dlay, g.dL, g.dwaves));
-        *chains_per_cu = blocks * g.dwaves * (64 / g.dL);
+        blocks = mh::delta_blocks_per_cu(s->room.rm.n, g.dwaves,
+                                         mh::delta_lds_bytes(s->geo.dlay, g.dwaves));
+        *chains_per_cu = blocks * g.dwaves;
     } else {
         blocks = mh::step_blocks_per_cu(g.L, g.npl, g.waves,
                                         mh::lds_bytes(s->geo.lay, g.L, g.waves));

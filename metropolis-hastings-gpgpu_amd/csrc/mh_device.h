@@ -174,10 +174,12 @@ inline MH_HD int bank_place(int o, unsigned* used) {
     return o;
 }
 
-// LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables as in
-// ChainLds plus three replay streams (areas, ones, zeros), then per chain the configuration and
-// every cached quantity a proposal changes only locally. The replay reads each ordered sum as a
-// stream of NP = round4(N + 1) entries, zero past its end (sentinels / zero fill).
+// LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables (object
+// and clearance records, the relationships' objects as int4 {s, t, as, at}; the relationship
+// records themselves stay in HBM) plus three replay streams (areas, ones, zeros), then per
+// chain the configuration and every cached quantity a proposal changes only locally that other
+// lanes read (rotY and the symmetry rows live in the owner lanes' registers). The replay reads
+// each ordered sum as a stream of NP = round4(N + 1) entries, zero past its end.
 struct DeltaLds {
     int hdr, h_obj, h_clr, h_rel, h_frz, h_room;
     int h_area, h_ones, h_zero;  // float[DL] areas, float[DL] ones, double[DL] zeros
@@ -185,10 +187,9 @@ struct DeltaLds {
     int NR;         // relationship stream length round4(max(R, 1))
     int DL;         // dense replay length max(NP, NR)
     int X, Y;       // double[NP] (zero past N)
-    int RY;         // double[N]
-    int P;          // float4[N] {xf, yf, rotYf, 0}
-    int CPH;        // float[NP] -cos(phi_i): FocalPoint terms
-    int RMX, RMA;   // float[2][NP] -(row max), int[2][NP] argmax: symmetry rows, cur/proposed
+    int P;          // float4[NP] {xf, yf, rotYf, -cos(phi)} (zero past N): the FocalPoint terms
+                    // are every fourth float of it
+    int NMX;        // float[NP] -(row max) of the proposed symmetry rows (the replay's stream)
     int CLA;        // float4[C] clearance boxes at their source objects
     int NZ;         // uint64[C][W] non-zero Clearance pairs (row = clearance, bit = object)
     int SAM, SAMB;  // uint32[SW] non-zero SurfaceArea entries (C clearances then N objects), backup
@@ -201,14 +202,16 @@ struct DeltaLds {
     int stride;     // bytes per chain
 };
 
-inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h_rel,
-                             int& h_frz, int& h_room);
-
 inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     DeltaLds l;
     const int np = (n + 1 + 3) & ~3;
     l.NP = np;
-    int h = room_header(n, c, r, l.h_obj, l.h_clr, l.h_rel, l.h_frz, l.h_room);
+    int h = 0;
+    l.h_obj = h;  h += round16((int)sizeof(ObjConst) * n);
+    l.h_clr = h;  h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
+    l.h_rel = h;  h += round16(16 * (r > 0 ? r : 1));
+    l.h_frz = h;  h += round16(n + 1);
+    l.h_room = h; h += round16((int)sizeof(DevRoom));
     l.NR = ((r > 1 ? r : 1) + 3) & ~3;
     l.DL = np > l.NR ? np : l.NR;
     l.h_area = h; h += round16(4 * l.DL);
@@ -225,11 +228,8 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     int o = 0;
     l.X = o;    o += 8 * np;
     l.Y = o;    o += 8 * np;
-    l.RY = o;   o += round16(8 * n);
-    l.P = o;    o += 16 * n;
-    l.CPH = o;  o += 4 * np;
-    l.RMX = o;  o += 4 * 2 * np;
-    l.RMA = o;  o += round16(4 * 2 * np);
+    l.P = o;    o += 16 * np;
+    l.NMX = o;  o += round16(4 * np);
     l.CLA = o;  o += 16 * (c > 0 ? c : 1);
     l.NZ = o;   o += 8 * l.W * (c > 0 ? c : 1);
     l.RPW = o;  o += 8 * nrp;
@@ -240,20 +240,9 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.LSA = o;  o += round16(4 * l.cap_sa);
     l.AUX = o;  o += 192;
     o = round16(o);
-    if ((o & 255) == 0) o += 16;  // spread the chains of one wave over the LDS banks
+    if ((o & 255) == 0) o += 16;  // spread the chains' arrays over the LDS banks
     l.stride = o;
     return l;
-}
-
-inline MH_HD int room_header(int n, int c, int r, int& h_obj, int& h_clr, int& h_rel,
-                             int& h_frz, int& h_room) {
-    int h = 0;
-    h_obj = h; h += round16((int)sizeof(ObjConst) * n);
-    h_clr = h; h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
-    h_rel = h; h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
-    h_frz = h; h += round16(n + 1);
-    h_room = h; h += round16((int)sizeof(DevRoom));
-    return h;
 }
 
 // Objects per lane of the full-evaluation kernel instance that serves npl (mh_chain.hip launch()).

@@ -186,8 +186,8 @@ def test_kernelwrapper_mh_seed(mh, hiplib, monkeypatch):
 STEP_PATHS = [  # (name, env): every RNG path a 64-object chain can take
     ("full L=64 WaveRng", {"MH_DELTA": "0"}),
     ("full L=32 ChainRng", {"MH_DELTA": "0", "MH_LANES": "32"}),
-    ("incremental", {"MH_DELTA": "1"}),
-    ("incremental L=64 WaveRng", {"MH_DELTA": "1", "MH_DELTA_LANES": "64"}),
+    ("incremental WaveRng", {"MH_DELTA": "1"}),
+    ("incremental WaveRng 1-chain workgroups", {"MH_DELTA": "1", "MH_DELTA_WAVES": "1"}),
 ]
 
 
@@ -226,14 +226,16 @@ def _crowded_room(mh, n):
     return room
 
 
-@pytest.mark.parametrize("lanes", ["64", "32"])
-def test_incremental_list_overflow_windows(mh, orc, hiplib, monkeypatch, lanes):
+@pytest.mark.parametrize("waves", ["", "3"])
+def test_incremental_list_overflow_windows(mh, orc, hiplib, monkeypatch, waves):
     """The incremental kernel sums Clearance / SurfaceArea lists longer than its LDS capacity
     (4*NP and NP terms, mh_device.h make_delta_layout) in windows rebuilt in place. Here all
     C*N Clearance pairs are non-zero at every step (C*N = 6,400 >> 4*NP = 768), so every
-    step takes that path; bit for bit against the oracle."""
+    step takes that path; bit for bit against the oracle (the default workgroup and a 3-chain
+    one, so chains of a workgroup run at different speeds)."""
     monkeypatch.setenv("MH_DELTA", "1")
-    monkeypatch.setenv("MH_DELTA_LANES", lanes)
+    if waves:
+        monkeypatch.setenv("MH_DELTA_WAVES", waves)
     n = 160
     room = _crowded_room(mh, n)
     c = room.srf.nClearances
@@ -241,14 +243,16 @@ def test_incremental_list_overflow_windows(mh, orc, hiplib, monkeypatch, lanes):
     assert c * n > 4 * np_pad  # the list cannot fit: windows on every step
     chains, steps, seed = 16, 120, 160
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == "incremental" and s.step_kernel()[0] == int(lanes)
+        assert s.step_kernel()[2] == "incremental" and s.step_kernel()[0] == 64
+        if waves:
+            assert s.step_kernel()[1] == int(waves)
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
     rp, rc, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS)
     # the final states still have (nearly) every pair non-zero, far past the capacity
     assert min(_nonzero_clearance_pairs(room, rp[k]) for k in range(chains)) > 4 * np_pad
-    check_chains(f"crowded N={n} incremental L={lanes}", pts, costs, rp, rc)
+    check_chains(f"crowded N={n} incremental waves={waves or 'default'}", pts, costs, rp, rc)
 
 
 def _nonzero_clearance_pairs(room, pts):

@@ -594,7 +594,6 @@ def test_wave_rng_window_overrun(mh, orc, hiplib, monkeypatch, step):
     regularly draw past WaveRng's 64-word window (the direct-draw fallback for words and
     normals). Bit for bit against the oracle, including across launch boundaries."""
     monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
-    monkeypatch.setenv("MH_DELTA_LANES", "64")  # one chain per wavefront: the WaveRng instance
     room = mh.synthetic_room(64)
     for i in range(61):
         room.cfg[i].frozen = True

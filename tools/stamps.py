@@ -30,7 +30,7 @@ def main():
         s.finalize()
         s.summary()
         lanes, cpw, s_kind = s.step_kernel()
-    out = (C.c_ulonglong * 12)()
+    out = (C.c_ulonglong * 14)()
     delta = hasattr(lib, "mh_debug_delta_cycles") and s_kind == "incremental"
     if delta:  # incremental step kernel: per-wavefront stamps, 64/lanes chains per wavefront
         assert lib.mh_debug_delta_cycles(out) == 0
@@ -47,10 +47,13 @@ def main():
         steps = chains * iters
         print(f"  rejection bound evaluated on {out[8] / steps:.4f} of steps, certain reject on "
               f"{out[9] / steps:.4f} ({out[9] / out[8]:.4f} of those evaluated)")
-    if delta:
+    if delta and out[12]:  # counts (MH_STAMPS=2 builds): per step that reached the replay
         steps = chains * iters
-        print(f"  mean Clearance list {out[8] / steps:.2f}, SurfaceArea list {out[9] / steps:.2f}, "
-              f"overflow fractions {out[10] / steps:.4f} / {out[11] / steps:.4f}")
+        rep = max(1, out[12] - out[13])
+        print(f"  rejection bound evaluated on {out[12] / steps:.4f} of steps, certain reject on "
+              f"{out[13] / steps:.4f}; per replayed step: mean Clearance list "
+              f"{out[8] / rep:.2f}, SurfaceArea list {out[9] / rep:.2f}, overflow fractions "
+              f"{out[10] / rep:.4f} / {out[11] / rep:.4f}")
 
 
 if __name__ == "__main__":
