@@ -680,7 +680,13 @@ __device__ __forceinline__ float list_walk(const float* fs, int from, int to, fl
     return a;
 }
 
-__device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r, float out[8]) {
+// (`dense`: diagnostic builds add the cycles of the dense walk to it)
+__device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r, float out[8],
+                       unsigned long long* dense = nullptr) {
+#if MH_STAMPS
+    unsigned long long t_in;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_in) :: "memory");
+#endif
     const DevRoom& rm = *ch.rm;
     const int k = r;
     const float* ms = ch.ONES;
@@ -724,6 +730,15 @@ __device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r
             accf = (double)(float)(accf + v[u]);
         }
     }
+#if MH_STAMPS
+    {
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t_out;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_out) :: "memory");
+        if (dense) *dense += t_out - t_in;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
     // Clearance / SurfaceArea lists longer than NP: their tails, then (lists longer than the
     // buffer, rare) further windows rebuilt in place.
     const int cnt = k == 4 ? cnt_cl : (k == 5 ? cnt_sa : 0);
@@ -1006,7 +1021,11 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             atomicAdd(&g_delta_counts[3], (unsigned long long)(cnt_sa > ch.cap_sa));
         }
 #endif
+#if MH_STAMPS
+        replay(ch, n, cnt_cl, cnt_sa, r, sc, &cyc[7]);
+#else
         replay(ch, n, cnt_cl, cnt_sa, r, sc);
+#endif
         DSTAMP(5);
         } else {
         DSTAMP(4);

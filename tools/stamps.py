@@ -14,7 +14,7 @@ os.environ.setdefault("MH_LIB", str(ROOT / "ablate" / "libmhgpu_stamps.so"))
 import __graft_entry__ as graft  # noqa: E402
 
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
-                "term lists", "replay", "accept/restore", "-"]
+                "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
 PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
           "E SA walk + CL list", "F PW/ANG + replay", "accept/undo"]
 
@@ -39,7 +39,7 @@ def main():
     else:
         assert lib.mh_debug_phase_cycles(out) == 0
         names, per, unit = PHASES, chains * iters, "cycles/chain-step"
-    tot = sum(out[:8])
+    tot = sum(out[:7] if delta else out[:8])  # (delta: [7] is a part of [5])
     print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes} delta={delta}")
     for name, v in zip(names, out[:8]):
         print(f"  {name:18s} {100.0 * v / tot:6.2f}%   {v / per:10.1f} {unit}")
