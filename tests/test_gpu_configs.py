@@ -2,6 +2,7 @@
 the reference edges that short runs do not reach -- each chain bit for bit against the oracle
 (oracle/mh_oracle.c, the restatement of KernelFolder/Kernel/Kernel.cu:754-828).
 
+* config 1: the console harness's 32-object room through KernelWrapper, 10,000 chains x 100 steps;
 * config 2: the 8-object room, all 1,024 chains x 10k steps;
 * config 3: 64 chains sampled by global id out of a 65,536-chain, 100k-step session;
 * config 4: one rank's shard (global ids 7*65,536 ...), the 2-rank bench.py launcher path, and
@@ -64,6 +65,19 @@ def _in_room(room, pts):
     w = np.float32(room.surface_rectangle[0].x)
     return bool(np.all((pts[..., 0] >= 0) & (pts[..., 0] <= w) & (pts[..., 1] >= 0) &
                        (pts[..., 1] <= w)))
+
+
+def test_config1_main_fixture_full_size(mh, orc, hiplib, monkeypatch):
+    """Config 1: the console harness's room (Kernel.cu:1007-1194, N=32) through
+    the reference's own symbol KernelWrapper, 10,000 chains x 100 steps = 1M samples, every
+    chain against the oracle ($MH_SEED stands in for time(NULL), Kernel.cu:943)."""
+    room = mh.main_fixture()
+    chains, steps, seed = 10_000, 100, 20_240_531
+    monkeypatch.setenv("MH_SEED", str(seed))
+    pts, costs = mh.kernel_wrapper(room, chains, steps)  # seed=None -> KernelWrapper
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS)
+    check_chains("config 1 (main() room N=32, 10000 x 100, KernelWrapper)", pts, costs,
+                 ref_pts, ref_costs, report=True)
 
 
 def test_config2_full_length(mh, orc, hiplib):
