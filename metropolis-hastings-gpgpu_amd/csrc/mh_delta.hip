@@ -61,11 +61,13 @@ struct Own {
     typedef double dvec __attribute__((ext_vector_type(S)));
     typedef float fvec __attribute__((ext_vector_type(S)));
     typedef int ivec __attribute__((ext_vector_type(S)));
+    typedef unsigned long long wvec __attribute__((ext_vector_type(S)));
     dvec ry;
     fvec cmx;
     ivec carg;
     fvec pmx;
     ivec parg;
+    wvec nz0;  // the non-zero Clearance pair words of clearance r (rows >= 64 live in LDS)
 };
 
 // v[m] = x where pred holds (m may differ between lanes).
@@ -97,7 +99,7 @@ struct DeltaAux {
 static_assert(sizeof(DeltaAux) <= 192, "DeltaAux");
 
 struct DeltaPtrs {
-    const ObjConst* objc;
+    const RectShape* objs;  // object off-limits rectangles
     const ClrConst* clrc;
     const int4* rel;        // LDS: relationship objects {s, t, as, at} (the hit test)
     const RelConst* relg;   // HBM: the relationship records (read for the ones a move touches)
@@ -108,7 +110,7 @@ struct DeltaPtrs {
     ObjP* P;      // {xf, yf, rotYf, -cos(phi)}, zero past N
     float* NMX;   // -(row max) of the proposed rows: the replay's Symmetry stream
     float4* CLA;
-    uint64_t* NZ;
+    uint64_t* NZ;  // pair words of clearances 64.. (the first 64 rows: registers, Own::nz0)
     uint32_t *SAM, *SAMB;
     double *RPW, *RANG;
     float *LCL, *LSA;
@@ -121,7 +123,7 @@ struct DeltaPtrs {
 
 __device__ __forceinline__ float4 obj_box(const DeltaPtrs& ch, int j) {
     const ObjP p = ch.P[j];
-    return shape_box(ch.objc[j].off, p.xf, p.yf);
+    return shape_box(ch.objs[j], p.xf, p.yf);
 }
 
 __device__ __forceinline__ float4 cla_box(const DeltaPtrs& ch, int ci) {
@@ -321,19 +323,27 @@ __device__ __forceinline__ void symmetry_delta(const DeltaPtrs& ch, Own<S>& o, i
 // ---- clearance pairs ------------------------------------------------------------------------
 
 // Row ci of the non-zero bit matrix from scratch (the lanes share the objects).
-__device__ void nz_row(const DeltaPtrs& ch, int n, int ci, int r) {
+template <int S>
+__device__ __forceinline__ void nz_row(const DeltaPtrs& ch, Own<S>& o, int n, int ci, int r) {
     const float4 A = ch.CLA[ci];
-    for (int w = 0; w < ch.W; ++w) {
+#pragma unroll
+    for (int w = 0; w < S; ++w) {
         const int j = w * 64 + r;
         const bool nz = j < n && overlap(A, obj_box(ch, j)) != 0.0f;
         const uint64_t word = __ballot(nz);
-        if (r == 0) ch.NZ[ci * ch.W + w] = word;
+        if (ci < 64) {
+            if (r == ci) o.nz0[w] = word;
+        } else if (r == 0) {
+            ch.NZ[(ci - 64) * S + w] = word;
+        }
     }
 }
 
 // Clearance boxes and pair bits after objects ka, kb changed (also restores them after a
 // rejected proposal has put the old poses back).
-__device__ void clearance_delta(const DeltaPtrs& ch, int n, int c, int ka, int kb, int r) {
+template <int S>
+__device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, int n, int c,
+                                                int ka, int kb, int r) {
     if (ka < 0 && kb < 0) return;
     uint64_t rows = 0;
     int t = 0;
@@ -346,17 +356,22 @@ __device__ void clearance_delta(const DeltaPtrs& ch, int n, int c, int ka, int k
     }
     wave_sync();
     // Columns ka, kb of the rows whose clearance did not move (lane-owned rows).
-    for (int s = 0; s < 2; ++s) {
-        const int j = s == 0 ? ka : kb;
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int j = s2 == 0 ? ka : kb;
         if (j < 0) continue;
         const float4 bj = obj_box(ch, j);
         const uint64_t bit = 1ull << (j & 63);
         t = 0;
         for (int ci = r; ci < c; ci += L, ++t) {
             if (rows & (1ull << t)) continue;
-            uint64_t* wd = &ch.NZ[ci * ch.W + (j >> 6)];
             const bool nz = overlap(ch.CLA[ci], bj) != 0.0f;
-            *wd = nz ? (*wd | bit) : (*wd & ~bit);
+            if (t == 0) {
+                const uint64_t w0 = o.nz0[j >> 6];
+                o.nz0[j >> 6] = nz ? (w0 | bit) : (w0 & ~bit);
+            } else {
+                uint64_t* wd = &ch.NZ[(ci - 64) * S + (j >> 6)];
+                *wd = nz ? (*wd | bit) : (*wd & ~bit);
+            }
         }
     }
     // Rows of the clearances that moved, one at a time.
@@ -365,7 +380,7 @@ __device__ void clearance_delta(const DeltaPtrs& ch, int n, int c, int ka, int k
         if (who == 0) break;
         const int b = __builtin_ctzll(who);
         const int tb = __builtin_amdgcn_readlane(rows ? __builtin_ctzll(rows) : 0, b);
-        nz_row(ch, n, tb * L + b, r);
+        nz_row<S>(ch, o, n, tb * L + b, r);
         if (r == b) rows &= rows - 1;
     }
 }
@@ -399,23 +414,30 @@ __device__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
 // Non-zero Clearance terms, clearance-major then object (Kernel.cu:408-431), negated: those at
 // positions [lo, lo + cap_cl) go to LCL[pos - lo]. Returns the total count. With `sum`, also
 // this lane's partial sum of the terms it evaluated and their count (the rejection bound).
-__device__ int build_cl_list(const DeltaPtrs& ch, int c, int r, int lo, float* sum = nullptr,
-                             int* cnt_own = nullptr) {
+template <int S>
+__device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& o, int c, int r,
+                                             int lo, float* sum = nullptr,
+                                             int* cnt_own = nullptr) {
     int base = 0;
     float acc = 0.0f;
     int own = 0;
     for (int cb = 0; cb < c; cb += L) {
         const int ci = cb + r;
+        uint64_t wd[S];
+#pragma unroll
+        for (int w = 0; w < S; ++w)
+            wd[w] = ci >= c ? 0ull : (cb == 0 ? (uint64_t)o.nz0[w] : ch.NZ[(ci - 64) * S + w]);
         int cnt = 0;
-        if (ci < c)
-            for (int w = 0; w < ch.W; ++w) cnt += __builtin_popcountll(ch.NZ[ci * ch.W + w]);
+#pragma unroll
+        for (int w = 0; w < S; ++w) cnt += __builtin_popcountll(wd[w]);
         int tot;
         int pos = base + group_excl_scan<L>(cnt, r, tot);
         own += cnt;
         if (cnt) {
             const float4 A = ch.CLA[ci];
-            for (int w = 0; w < ch.W; ++w) {
-                uint64_t word = ch.NZ[ci * ch.W + w];
+#pragma unroll
+            for (int w = 0; w < S; ++w) {
+                uint64_t word = wd[w];
                 while (word) {
                     const int j = w * 64 + __builtin_ctzll(word);
                     word &= word - 1;
@@ -681,8 +703,10 @@ __device__ __forceinline__ float list_walk(const float* fs, int from, int to, fl
 }
 
 // (`dense`: diagnostic builds add the cycles of the dense walk to it)
-__device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r, float out[8],
-                       unsigned long long* dense = nullptr) {
+template <int S>
+__device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int n, int cnt_cl,
+                                       int cnt_sa, int r, float out[8],
+                                       unsigned long long* dense = nullptr) {
 #if MH_STAMPS
     unsigned long long t_in;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_in) :: "memory");
@@ -705,7 +729,8 @@ __device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r
     } else if (k == 4) {
         fs = ch.LCL;
     } else if (k == 5) {
-        fs = ch.LSA;
+        fs = ch.LSA;  // (its capacity may be below NP: the stream ends at the zero-filled end)
+        lim = (min(cnt_sa, ch.cap_sa) + 3) & ~3;
     } else if (k == 6) {
         ds = ch.RPW;
         lim = ch.NR;
@@ -723,7 +748,9 @@ __device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            v[u] = (double)msl[l0 + u] * dsl[l0 + u] + (double)fsl[u * st];
+            // one rounding either way: rn(m * d) where f = 0 (VisualBalance: m = area) and
+            // rn(d + f) where m = 1 (every other sum), so the fused form is the two-step one
+            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fsl[u * st]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];
@@ -745,10 +772,11 @@ __device__ void replay(const DeltaPtrs& ch, int n, int cnt_cl, int cnt_sa, int r
     const int cap = k == 4 ? ch.cap_cl : ch.cap_sa;
     float af = (float)accf;
     const int tail = (min(cnt, cap) + 3) & ~3;
-    if (tail > ch.NP) af = list_walk(fs, ch.NP, tail, af);
+    const int walked = min(lim, ch.DL);  // what the dense walk covered of this lane's stream
+    if (tail > walked) af = list_walk(fs, walked, tail, af);
     for (int lo = ch.cap_cl; lo < cnt_cl; lo += ch.cap_cl) {
         wave_sync();
-        build_cl_list(ch, rm.c, r, lo);
+        build_cl_list<S>(ch, o, rm.c, r, lo);
         const int m = min(ch.cap_cl, cnt_cl - lo);
         for (int l = m + r; l < ((m + 3) & ~3); l += L) ch.LCL[l] = 0.0f;
         wave_sync();
@@ -804,12 +832,12 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int waves_per_wg = blockDim.x >> 6;
 
-    ObjConst* objc_l = reinterpret_cast<ObjConst*>(lds + lay.h_obj);
+    RectShape* objs_l = reinterpret_cast<RectShape*>(lds + lay.h_obj);
     ClrConst* clrc_l = reinterpret_cast<ClrConst*>(lds + lay.h_clr);
     int4* rel_l = reinterpret_cast<int4*>(lds + lay.h_rel);
     unsigned char* frozen = lds + lay.h_frz;
     DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + lay.h_room);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) objc_l[i] = a.objc[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) objs_l[i] = a.objc[i].off;
     for (int i = threadIdx.x; i < c; i += blockDim.x) clrc_l[i] = a.clrc[i];
     for (int i = threadIdx.x; i < nr; i += blockDim.x)
         rel_l[i] = make_int4(a.relc[i].s, a.relc[i].t, a.relc[i].as, a.relc[i].at);
@@ -836,7 +864,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(boff) : "v"(boff));
     unsigned char* base = lds + boff;
     DeltaPtrs ch;
-    ch.objc = objc_l;
+    ch.objs = objs_l;
     ch.clrc = clrc_l;
     ch.rel = rel_l;
     ch.relg = a.relc;
@@ -877,6 +905,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         o.ry[t] = 0.0;
         o.cmx[t] = o.pmx[t] = 0.0f;
         o.carg[t] = o.parg[t] = -1;
+        o.nz0[t] = 0ull;
         const int i = t * L + r;
         if (i < n) o.ry[t] = src[F_RY * n + i];
     }
@@ -916,7 +945,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         if (nonzero4(sa_entry(ch, c, e))) sam_put(ch, e, true);
     for (int ci = r; ci < c; ci += L) ch.CLA[ci] = cla_box(ch, ci);
     wave_sync();
-    for (int ci = 0; ci < c; ++ci) nz_row(ch, n, ci, r);
+    for (int ci = 0; ci < c; ++ci) nz_row<S>(ch, o, n, ci, r);
     rels_delta(ch, nr, -2, -1, r);
     for (int i = 0; i < n; ++i) {
         const RowMax s = scan_row<S>(ch, o, n, i, wild_cnt > 0, r);
@@ -957,7 +986,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             if (k >= 0) {
                 const ObjP p = ch.P[k];
                 ch.P[k].pad = -focal_cos(*rm_l, p);
-                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.objc[k].off, p.xf, p.yf))));
+                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.objs[k], p.xf, p.yf))));
                 if (k < c)
                     sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrc[k].shape, p.xf, p.yf))));
                 const DBackup& ob = ch.aux->b[r];
@@ -968,7 +997,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         const int wild_star = wild_cnt + __shfl(dwild, 0) + __shfl(dwild, 1);
         wave_sync();
         DSTAMP(0);
-        clearance_delta(ch, n, c, ka, kb, r);
+        clearance_delta<S>(ch, o, n, c, ka, kb, r);
         DSTAMP(1);
         rels_delta(ch, nr, ka, kb, r);
         DSTAMP(2);
@@ -983,7 +1012,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         float u_acc = 0.0f;
         float clsum = 0.0f, sasum = 0.0f;
         int kcl = 0;
-        const int cnt_cl = build_cl_list(ch, c, r, 0, &clsum, &kcl);
+        const int cnt_cl = build_cl_list<S>(ch, o, c, r, 0, &clsum, &kcl);
         const int cnt_sa = build_sa_list(ch, n, c, r, 0, &sasum);
         if constexpr (FASTD) {
             u_acc = rng.uniform();
@@ -1003,7 +1032,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         if (!fast_rej) {
         // zero past each list's end: to NP for the dense walk, to round4 for the list walk
         const int zcl = max(np, (min(cnt_cl, ch.cap_cl) + 3) & ~3);
-        const int zsa = max(np, (min(cnt_sa, ch.cap_sa) + 3) & ~3);
+        const int zsa = (min(cnt_sa, ch.cap_sa) + 3) & ~3;  // (lane 5's dense stream ends there)
         for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) ch.LCL[l] = 0.0f;
         for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) ch.LSA[l] = 0.0f;
 #pragma unroll
@@ -1022,9 +1051,9 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         }
 #endif
 #if MH_STAMPS
-        replay(ch, n, cnt_cl, cnt_sa, r, sc, &cyc[7]);
+        replay<S>(ch, o, n, cnt_cl, cnt_sa, r, sc, &cyc[7]);
 #else
-        replay(ch, n, cnt_cl, cnt_sa, r, sc);
+        replay<S>(ch, o, n, cnt_cl, cnt_sa, r, sc);
 #endif
         DSTAMP(5);
         } else {
@@ -1062,7 +1091,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             }
             for (int w = r; w < ch.SW; w += L) ch.SAM[w] = ch.SAMB[w];
             wave_sync();
-            clearance_delta(ch, n, c, ka, kb, r);
+            clearance_delta<S>(ch, o, n, c, ka, kb, r);
             rels_delta(ch, nr, ka, kb, r);
             wave_sync();
         }

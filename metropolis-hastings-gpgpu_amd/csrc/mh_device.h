@@ -175,7 +175,7 @@ inline MH_HD int bank_place(int o, unsigned* used) {
 }
 
 // LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables (object
-// and clearance records, the relationships' objects as int4 {s, t, as, at}; the relationship
+// rectangles and clearance records, the relationships' objects as int4 {s, t, as, at}; the relationship
 // records themselves stay in HBM) plus three replay streams (areas, ones, zeros), then per
 // chain the configuration and every cached quantity a proposal changes only locally that other
 // lanes read (rotY and the symmetry rows live in the owner lanes' registers). The replay reads
@@ -191,13 +191,14 @@ struct DeltaLds {
                     // are every fourth float of it
     int NMX;        // float[NP] -(row max) of the proposed symmetry rows (the replay's stream)
     int CLA;        // float4[C] clearance boxes at their source objects
-    int NZ;         // uint64[C][W] non-zero Clearance pairs (row = clearance, bit = object)
+    int NZ;         // uint64[C - 64][W] non-zero Clearance pairs of clearances 64.. (row =
+                    // clearance, bit = object; rows 0..63 live in the owner lanes' registers)
     int SAM, SAMB;  // uint32[SW] non-zero SurfaceArea entries (C clearances then N objects), backup
     int RPW, RANG;  // double[NR] negated PairWise / PairWiseAngle terms (zero past R)
     int LCL, LSA;   // float[cap] compacted negated Clearance / SurfaceArea terms (zero filled
-                    // to max(NP, round4(count)))
+                    // to round4(count))
     int AUX;        // per-chain scalars (backups, current costs)
-    int W, SW;      // words per NZ row, SAM words
+    int W, SW;      // words per NZ row (the kernel's object slots), SAM words
     int cap_cl, cap_sa;
     int stride;     // bytes per chain
 };
@@ -207,7 +208,7 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     const int np = (n + 1 + 3) & ~3;
     l.NP = np;
     int h = 0;
-    l.h_obj = h;  h += round16((int)sizeof(ObjConst) * n);
+    l.h_obj = h;  h += round16((int)sizeof(RectShape) * n);
     l.h_clr = h;  h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
     l.h_rel = h;  h += round16(16 * (r > 0 ? r : 1));
     l.h_frz = h;  h += round16(n + 1);
@@ -218,12 +219,13 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.h_ones = h; h += round16(4 * l.DL);
     l.h_zero = h; h += round16(8 * l.DL);
     l.hdr = h;
-    l.W = (n + 63) / 64;
+    l.W = n <= 64 ? 1 : n <= 128 ? 2 : n <= 256 ? 4 : 8;  // the kernel instance's object slots
     l.SW = (c + n + 31) / 32;
     // Clearance list capacity: the non-zero pairs of a sampled room run to ~4 per object at
     // N = 128..256 (tools/stamps.py counts build); longer lists are summed in windows.
     l.cap_cl = 4 * np < 32 ? 32 : 4 * np;
-    l.cap_sa = np < 32 ? 32 : np;
+    // SurfaceArea list: a few dozen non-zero terms in sampled rooms (18 at N = 256), so NP / 4.
+    l.cap_sa = np / 4 < 32 ? 32 : ((np / 4 + 3) & ~3);
     const int nrp = l.NR;
     int o = 0;
     l.X = o;    o += 8 * np;
@@ -231,7 +233,7 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.P = o;    o += 16 * np;
     l.NMX = o;  o += round16(4 * np);
     l.CLA = o;  o += 16 * (c > 0 ? c : 1);
-    l.NZ = o;   o += 8 * l.W * (c > 0 ? c : 1);
+    l.NZ = o;   o += 8 * l.W * (c > 64 ? c - 64 : 1);  // rows 64..: the first 64 are registers
     l.RPW = o;  o += 8 * nrp;
     l.RANG = o; o += round16(8 * nrp);
     l.SAM = o;  o += 4 * l.SW;
