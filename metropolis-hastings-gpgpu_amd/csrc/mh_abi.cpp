@@ -227,7 +227,8 @@ struct Geometry {
 
 // Incremental step kernel geometry: one chain per wavefront; the workgroup size (chains per
 // workgroup, up to 12) that keeps the most chains resident per CU, as the runtime's occupancy
-// calculator counts them (registers, LDS, waves); ties go to fewer waves per workgroup. The
+// calculator counts them (registers, LDS, waves), rounded down to whole waves per SIMD above
+// four; ties go to fewer waves per workgroup. The
 // kernel is latency-bound, so resident chains are its throughput (measured at N = 256: 1 to 5
 // chains per CU gave 6.6e6 to 3.3e7 chain-steps/s, the launch time unchanged). It is the
 // default step above N = 128 (measured, chain-steps/s full vs incremental: N = 100 1.21e8 /
@@ -245,7 +246,10 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
         if (want_w && w != want_w) continue;
         const size_t b = mh::delta_lds_bytes(g.dlay, w);
         if (b > (size_t)max_lds) continue;
-        const int chains = mh::delta_blocks_per_cu(n, w, b) * w;
+        int chains = mh::delta_blocks_per_cu(n, w, b) * w;
+        // Whole waves per SIMD: a workgroup of 9 puts three chains on one SIMD, whose VALU then
+        // paces the other eight (N = 256: 9 chains 6.16e7 chain-steps/s, 8 chains 6.59e7).
+        if (!want_w && chains > 4) chains &= ~3;
         if (chains > best_chains) {
             best_chains = chains;
             g.dwaves = w;

@@ -68,6 +68,7 @@ struct Own {
     fvec pmx;
     ivec parg;
     wvec nz0;  // the non-zero Clearance pair words of clearance r (rows >= 64 live in LDS)
+    float4 cla0;  // clearance r's box at its source object (clearances >= 64: LDS)
 };
 
 // v[m] = x where pred holds (m may differ between lanes).
@@ -96,12 +97,12 @@ struct DeltaAux {
     int pad0;
     float cur[8];  // resultCosts of the current configuration
 };
-static_assert(sizeof(DeltaAux) <= 192, "DeltaAux");
+static_assert(sizeof(DeltaAux) <= kDeltaAuxBytes, "DeltaAux");
 
 struct DeltaPtrs {
     const RectShape* objs;  // object off-limits rectangles
-    const ClrConst* clrc;
-    const int4* rel;        // LDS: relationship objects {s, t, as, at} (the hit test)
+    const RectShape* clrs;  // clearance rectangles, the source object in .pad
+    const uint2* rel;       // LDS: relationship objects {s | t << 16, as | at << 16} (hit test)
     const RelConst* relg;   // HBM: the relationship records (read for the ones a move touches)
     const DevRoom* rm;
     const float *AREA, *ONES;  // replay streams shared by the workgroup
@@ -109,7 +110,7 @@ struct DeltaPtrs {
     double *X, *Y;
     ObjP* P;      // {xf, yf, rotYf, -cos(phi)}, zero past N
     float* NMX;   // -(row max) of the proposed rows: the replay's Symmetry stream
-    float4* CLA;
+    float4* CLA;  // boxes of clearances 64.. (the first 64: registers, Own::cla0)
     uint64_t* NZ;  // pair words of clearances 64.. (the first 64 rows: registers, Own::nz0)
     uint32_t *SAM, *SAMB;
     double *RPW, *RANG;
@@ -127,9 +128,20 @@ __device__ __forceinline__ float4 obj_box(const DeltaPtrs& ch, int j) {
 }
 
 __device__ __forceinline__ float4 cla_box(const DeltaPtrs& ch, int ci) {
-    const ClrConst& cc = ch.clrc[ci];
-    const ObjP p = ch.P[cc.src];
-    return shape_box(cc.shape, p.xf, p.yf);
+    const RectShape& cs = ch.clrs[ci];
+    const ObjP p = ch.P[cs.pad];
+    return shape_box(cs, p.xf, p.yf);
+}
+
+// Clearance ci's box: its owner lane's register (ci < 64) or LDS. `own`: this lane owns ci.
+template <int S>
+__device__ __forceinline__ float4 cla_get(const DeltaPtrs& ch, const Own<S>& o, int ci) {
+    return ci < 64 ? o.cla0 : ch.CLA[ci - 64];
+}
+template <int S>
+__device__ __forceinline__ void cla_put(const DeltaPtrs& ch, Own<S>& o, int ci, float4 v) {
+    if (ci < 64) o.cla0 = v;
+    else ch.CLA[ci - 64] = v;
 }
 
 // SurfaceAreaCosts entry e (Kernel.cu:453-480): clearance e's box at cfg[e] (the reference's
@@ -137,7 +149,7 @@ __device__ __forceinline__ float4 cla_box(const DeltaPtrs& ch, int ci) {
 __device__ __forceinline__ float4 sa_entry(const DeltaPtrs& ch, int c, int e) {
     if (e < c) {
         const ObjP p = ch.P[e];
-        return comp_overlaps(*ch.rm, shape_box(ch.clrc[e].shape, p.xf, p.yf));
+        return comp_overlaps(*ch.rm, shape_box(ch.clrs[e], p.xf, p.yf));
     }
     return comp_overlaps(*ch.rm, obj_box(ch, e - c));
 }
@@ -325,7 +337,15 @@ __device__ __forceinline__ void symmetry_delta(const DeltaPtrs& ch, Own<S>& o, i
 // Row ci of the non-zero bit matrix from scratch (the lanes share the objects).
 template <int S>
 __device__ __forceinline__ void nz_row(const DeltaPtrs& ch, Own<S>& o, int n, int ci, int r) {
-    const float4 A = ch.CLA[ci];
+    float4 A;  // (ci is wave-uniform)
+    if (ci < 64) {
+        A.x = grp_get<L>(o.cla0.x, ci, 0);
+        A.y = grp_get<L>(o.cla0.y, ci, 0);
+        A.z = grp_get<L>(o.cla0.z, ci, 0);
+        A.w = grp_get<L>(o.cla0.w, ci, 0);
+    } else {
+        A = ch.CLA[ci - 64];
+    }
 #pragma unroll
     for (int w = 0; w < S; ++w) {
         const int j = w * 64 + r;
@@ -348,9 +368,9 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
     uint64_t rows = 0;
     int t = 0;
     for (int ci = r; ci < c; ci += L, ++t) {
-        const int src = ch.clrc[ci].src;
+        const int src = ch.clrs[ci].pad;
         if (src == ka || src == kb) {
-            ch.CLA[ci] = cla_box(ch, ci);
+            cla_put<S>(ch, o, ci, cla_box(ch, ci));
             rows |= 1ull << t;
         }
     }
@@ -364,7 +384,7 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
         t = 0;
         for (int ci = r; ci < c; ci += L, ++t) {
             if (rows & (1ull << t)) continue;
-            const bool nz = overlap(ch.CLA[ci], bj) != 0.0f;
+            const bool nz = overlap(cla_get<S>(ch, o, ci), bj) != 0.0f;
             if (t == 0) {
                 const uint64_t w0 = o.nz0[j >> 6];
                 o.nz0[j >> 6] = nz ? (w0 | bit) : (w0 & ~bit);
@@ -392,9 +412,11 @@ __device__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
     uint64_t pend = 0;
     int t = 0;
     for (int q = r; q < nr; q += L, ++t) {
-        const int4 o = ch.rel[q];
-        const bool hit = ka == -2 || o.x == ka || o.y == ka || o.z == ka || o.w == ka ||
-                         (kb >= 0 && (o.x == kb || o.y == kb || o.z == kb || o.w == kb));
+        const uint2 w = ch.rel[q];
+        const int s0 = (int)(w.x & 0xffffu), t0 = (int)(w.x >> 16);
+        const int s1 = (int)(w.y & 0xffffu), t1 = (int)(w.y >> 16);
+        const bool hit = ka == -2 || s0 == ka || t0 == ka || s1 == ka || t1 == ka ||
+                         (kb >= 0 && (s0 == kb || t0 == kb || s1 == kb || t1 == kb));
         if (hit) pend |= 1ull << t;
     }
     while (__ballot(pend != 0)) {
@@ -434,7 +456,7 @@ __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& 
         int pos = base + group_excl_scan<L>(cnt, r, tot);
         own += cnt;
         if (cnt) {
-            const float4 A = ch.CLA[ci];
+            const float4 A = cla_get<S>(ch, o, ci);
 #pragma unroll
             for (int w = 0; w < S; ++w) {
                 uint64_t word = wd[w];
@@ -833,14 +855,19 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     const int waves_per_wg = blockDim.x >> 6;
 
     RectShape* objs_l = reinterpret_cast<RectShape*>(lds + lay.h_obj);
-    ClrConst* clrc_l = reinterpret_cast<ClrConst*>(lds + lay.h_clr);
-    int4* rel_l = reinterpret_cast<int4*>(lds + lay.h_rel);
+    RectShape* clrs_l = reinterpret_cast<RectShape*>(lds + lay.h_clr);
+    uint2* rel_l = reinterpret_cast<uint2*>(lds + lay.h_rel);
     unsigned char* frozen = lds + lay.h_frz;
     DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + lay.h_room);
     for (int i = threadIdx.x; i < n; i += blockDim.x) objs_l[i] = a.objc[i].off;
-    for (int i = threadIdx.x; i < c; i += blockDim.x) clrc_l[i] = a.clrc[i];
+    for (int i = threadIdx.x; i < c; i += blockDim.x) {
+        RectShape cs = a.clrc[i].shape;
+        cs.pad = a.clrc[i].src;
+        clrs_l[i] = cs;
+    }
     for (int i = threadIdx.x; i < nr; i += blockDim.x)
-        rel_l[i] = make_int4(a.relc[i].s, a.relc[i].t, a.relc[i].as, a.relc[i].at);
+        rel_l[i] = make_uint2((unsigned)a.relc[i].s | ((unsigned)a.relc[i].t << 16),
+                              (unsigned)a.relc[i].as | ((unsigned)a.relc[i].at << 16));
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     if (threadIdx.x == 0) *rm_l = a.rm;
     {
@@ -865,7 +892,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     unsigned char* base = lds + boff;
     DeltaPtrs ch;
     ch.objs = objs_l;
-    ch.clrc = clrc_l;
+    ch.clrs = clrs_l;
     ch.rel = rel_l;
     ch.relg = a.relc;
     ch.rm = rm_l;
@@ -906,6 +933,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         o.cmx[t] = o.pmx[t] = 0.0f;
         o.carg[t] = o.parg[t] = -1;
         o.nz0[t] = 0ull;
+        o.cla0 = make_float4(0.f, 0.f, 0.f, 0.f);
         const int i = t * L + r;
         if (i < n) o.ry[t] = src[F_RY * n + i];
     }
@@ -943,7 +971,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     int wild_cnt = group_sum<L>(wild);
     for (int e = r; e < c + n; e += L)
         if (nonzero4(sa_entry(ch, c, e))) sam_put(ch, e, true);
-    for (int ci = r; ci < c; ci += L) ch.CLA[ci] = cla_box(ch, ci);
+    for (int ci = r; ci < c; ci += L) cla_put<S>(ch, o, ci, cla_box(ch, ci));
     wave_sync();
     for (int ci = 0; ci < c; ++ci) nz_row<S>(ch, o, n, ci, r);
     rels_delta(ch, nr, -2, -1, r);
@@ -988,7 +1016,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
                 ch.P[k].pad = -focal_cos(*rm_l, p);
                 sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.objs[k], p.xf, p.yf))));
                 if (k < c)
-                    sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrc[k].shape, p.xf, p.yf))));
+                    sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrs[k], p.xf, p.yf))));
                 const DBackup& ob = ch.aux->b[r];
                 dwild = (wild_pose(ch.X[k], ch.Y[k], r == 0 ? rka : rkb) ? 1 : 0) -
                         (wild_pose(ob.x, ob.y, ob.ry) ? 1 : 0);

@@ -175,7 +175,7 @@ inline MH_HD int bank_place(int o, unsigned* used) {
 }
 
 // LDS carve-up of the incremental step kernel (mh_delta.hip): per-workgroup room tables (object
-// rectangles and clearance records, the relationships' objects as int4 {s, t, as, at}; the relationship
+// and clearance rectangles, the relationships' objects as 16-bit pairs {s, t, as, at}; the relationship
 // records themselves stay in HBM) plus three replay streams (areas, ones, zeros), then per
 // chain the configuration and every cached quantity a proposal changes only locally that other
 // lanes read (rotY and the symmetry rows live in the owner lanes' registers). The replay reads
@@ -190,7 +190,8 @@ struct DeltaLds {
     int P;          // float4[NP] {xf, yf, rotYf, -cos(phi)} (zero past N): the FocalPoint terms
                     // are every fourth float of it
     int NMX;        // float[NP] -(row max) of the proposed symmetry rows (the replay's stream)
-    int CLA;        // float4[C] clearance boxes at their source objects
+    int CLA;        // float4[C - 64] boxes of clearances 64.. at their source objects (the first
+                    // 64 live in the owner lanes' registers)
     int NZ;         // uint64[C - 64][W] non-zero Clearance pairs of clearances 64.. (row =
                     // clearance, bit = object; rows 0..63 live in the owner lanes' registers)
     int SAM, SAMB;  // uint32[SW] non-zero SurfaceArea entries (C clearances then N objects), backup
@@ -203,14 +204,16 @@ struct DeltaLds {
     int stride;     // bytes per chain
 };
 
+constexpr int kDeltaAuxBytes = 112;  // mh_delta.hip DeltaAux: two undo records, the current costs
+
 inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     DeltaLds l;
     const int np = (n + 1 + 3) & ~3;
     l.NP = np;
     int h = 0;
     l.h_obj = h;  h += round16((int)sizeof(RectShape) * n);
-    l.h_clr = h;  h += round16((int)sizeof(ClrConst) * (c > 0 ? c : 1));
-    l.h_rel = h;  h += round16(16 * (r > 0 ? r : 1));
+    l.h_clr = h;  h += round16((int)sizeof(RectShape) * (c > 0 ? c : 1));
+    l.h_rel = h;  h += round16(8 * (r > 0 ? r : 1));
     l.h_frz = h;  h += round16(n + 1);
     l.h_room = h; h += round16((int)sizeof(DevRoom));
     l.NR = ((r > 1 ? r : 1) + 3) & ~3;
@@ -232,7 +235,7 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.Y = o;    o += 8 * np;
     l.P = o;    o += 16 * np;
     l.NMX = o;  o += round16(4 * np);
-    l.CLA = o;  o += 16 * (c > 0 ? c : 1);
+    l.CLA = o;  o += 16 * (c > 64 ? c - 64 : 1);  // clearances 64.. (the first 64: registers)
     l.NZ = o;   o += 8 * l.W * (c > 64 ? c - 64 : 1);  // rows 64..: the first 64 are registers
     l.RPW = o;  o += 8 * nrp;
     l.RANG = o; o += round16(8 * nrp);
@@ -240,7 +243,7 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.SAMB = o; o += round16(4 * l.SW);
     l.LCL = o;  o += 4 * l.cap_cl;
     l.LSA = o;  o += round16(4 * l.cap_sa);
-    l.AUX = o;  o += 192;
+    l.AUX = o;  o += kDeltaAuxBytes;
     o = round16(o);
     if ((o & 255) == 0) o += 16;  // spread the chains' arrays over the LDS banks
     l.stride = o;
