@@ -26,8 +26,7 @@
 #endif
 #ifndef MH_DOUBLE
 #define MH_DOUBLE 0  // cost-probe builds: run phase k twice when bit k is set; product = 0
-                     // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay,
-                     // 128 incremental Clearance pairs, 256 rejection bound)
+                     // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay)
 #endif
 #define MH_REPS(bit) ((MH_DOUBLE & (bit)) ? 2 : 1)
 #define MH_CLOBBER() asm volatile("" ::: "memory")
@@ -644,18 +643,11 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
     // clearances its latency is lower, and those rooms run few chains).
     constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
     int cl_total = 0;
-    if constexpr (INC_CL)
-        for (int rep = 0; rep < MH_REPS(128); ++rep) {
-            MH_CLOBBER();
-            cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo);
-        }
+    if constexpr (INC_CL) cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo);
     if (r == 0) MH_PHASE(ch, 3, t0);
     if constexpr (FAST) {
         static_assert(INC_CL && L == 64, "the rejection bound needs one chain per wavefront");
-        bool rej = false;
-        for (int rep = 0; rep < MH_REPS(256); ++rep)
         if (rm.r <= L) {  // every relationship term is held by a lane (rpw[0], rang[0])
-            MH_CLOBBER();
             float clsum = 0.0f;  // this lane's object against the clearances it overlaps
             uint64_t bits = r < n ? clo.cm : 0ull;
             const int kcl = __builtin_popcountll(bits);
@@ -680,9 +672,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
             bt.ang = -(float)rang[0];
             bt.aang = fabsf(bt.ang);
             bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
-            rej = certain_reject(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total);
-        }
-        if (rm.r <= L) {
+            const bool rej = certain_reject(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total);
             if (r == 0) MH_PHASE(ch, 4, t0);
 #if MH_STAMPS
             if (r == 0) {

@@ -8,8 +8,8 @@ import os
 from collections import defaultdict
 
 NAMES = {"2": "ablate per-object atan2/cos", "16": "ablate PW/ANG terms", "dbl1": "A per-object",
-         "dbl2": "B full symmetry", "dbl64": "B delta symmetry", "dbl128": "C Clearance pairs",
-         "dbl256": "D rejection bound", "dbl4": "E surface area walk", "dbl8": "E clearance",
+         "dbl2": "B full symmetry", "dbl64": "B delta symmetry",
+         "dbl4": "E surface area walk", "dbl8": "E clearance",
          "dbl16": "F pairwise appends", "dbl32": "G replay"}
 
 
