@@ -817,11 +817,13 @@ __device__ __forceinline__ double rel_angle(const RelConst& rc, double tp, float
     return on ? fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm : 0.0;
 }
 
-__device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, double& tpw,
-                                          double& tang) {
+// `pose(k)` gives object k's float pose words (ObjP: xf, yf, rotYf).
+template <class PoseOf>
+__device__ __forceinline__ void rel_terms_of(const RelConst& rc, PoseOf pose, double& tpw,
+                                             double& tang) {
     tpw = 0.0;
     tang = 0.0;
-    const ObjP ps = P[rc.s], pt = P[rc.t];
+    const ObjP ps = pose(rc.s), pt = pose(rc.t);
     const double d = distance_f(ps.xf, ps.yf, pt.xf, pt.yf);
     // d / start below the range, end / d above it: one division for either side
     const bool below = d < rc.start, above = d > rc.end;
@@ -829,7 +831,7 @@ __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, dou
         const double f = (below ? d : rc.end) / (below ? rc.start : d);
         tpw = f * f;
     }
-    const ObjP as = P[rc.as], at = P[rc.at];
+    const ObjP as = pose(rc.as), at = pose(rc.at);
     const double th = theta_f(as.xf, as.yf, at.xf, at.yf, at.rotYf);
     bool on;
     double norm;
@@ -842,6 +844,11 @@ __device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, dou
         norm = rc.norm_n;
     }
     if (on) tang = fmin(fabs(th - rc.amin), fabs(th - rc.amax)) / norm;
+}
+
+__device__ __forceinline__ void rel_terms(const RelConst& rc, const ObjP* P, double& tpw,
+                                          double& tang) {
+    rel_terms_of(rc, [P](int k) { return P[k]; }, tpw, tang);
 }
 
 // ---- proposal draws and the accept rule ----------------------------------------------------

@@ -4,7 +4,7 @@
 // of Costs() (Kernel.cu:516-550) is the same before and after it. This kernel keeps, per chain,
 // every quantity a proposal can only change locally, recomputes just the affected entries, and
 // replays the reference's ordered float/double sums from the cached terms:
-//   * FocalPoint: -cos(phi_i) per object (the .pad word of the object's pose record in LDS);
+//   * FocalPoint: -cos(phi_i) per object (an LDS stream, the replay reads it as it lies);
 //   * Symmetry: each row's exact maximum and its argmax, in the row owner's registers (current
 //     and proposed); a proposal re-scans the changed rows and folds the changed columns into
 //     the others;
@@ -22,7 +22,7 @@
 // ceil(N / 64)). The kernel is latency-bound (a step is a chain of short dependent passes), so
 // its throughput is the number of chains a CU keeps resident, and that is set by LDS per chain:
 // whatever only the owner lane reads (rotY, the symmetry rows) lives in registers, and LDS holds
-// what other lanes read (float poses, boxes, pair bits) and the replay streams.
+// what other lanes read (poses, object and clearance boxes, pair bits) and the replay streams.
 
 #include <stdint.h>
 #include <stdlib.h>
@@ -52,7 +52,7 @@ struct RowMax {  // one symmetry row: exact max(0, max_j value) and the j attain
     int arg;
 };
 
-// Registers of one chain, per owner lane: rotY of objects r + 64 s and the symmetry rows
+// Registers of one chain, per owner lane: the pose of objects r + 64 s and the symmetry rows
 // (current configuration; proposed configuration). Vector types, so that no access -- not even
 // one whose slot differs between lanes -- sends them to scratch: an array of S elements indexed
 // by a select chain was folded into an indexed load of a stack slot.
@@ -63,6 +63,7 @@ struct Own {
     typedef int ivec __attribute__((ext_vector_type(S)));
     typedef unsigned long long wvec __attribute__((ext_vector_type(S)));
     dvec ry;
+    fvec xf, yf;  // (float)x, (float)y
     fvec cmx;
     ivec carg;
     fvec pmx;
@@ -78,6 +79,10 @@ __device__ __forceinline__ void slot_put(V& v, int m, T x, bool pred) {
     for (int q = 0; q < S; ++q) v[q] = (pred && q == m) ? x : v[q];
 }
 
+__device__ __forceinline__ float uniform_f(float v) {  // (v is wave-uniform)
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 // rotY of object k (wave-uniform k), from its owner lane.
 template <int S>
 __device__ __forceinline__ double obj_ry(const Own<S>& o, int k) {
@@ -90,12 +95,11 @@ struct DBackup {  // an object's cost-relevant pose and FocalPoint term before a
     double x, y, ry;
 };
 
-struct DeltaAux {
+struct DeltaAux {  // (the current configuration's resultCosts live in registers)
     DBackup b[2];
     int nb;
     int swap_a, swap_b;
     int pad0;
-    float cur[8];  // resultCosts of the current configuration
 };
 static_assert(sizeof(DeltaAux) <= kDeltaAuxBytes, "DeltaAux");
 
@@ -108,7 +112,9 @@ struct DeltaPtrs {
     const float *AREA, *ONES;  // replay streams shared by the workgroup
     const double* ZERO;
     double *X, *Y;
-    ObjP* P;      // {xf, yf, rotYf, -cos(phi)}, zero past N
+    float4* BOX;  // object off-limits boxes at the current poses, zero past N
+    float* RYF;   // (float)rotY
+    float* CPH;   // -cos(phi): the FocalPoint terms (the replay's stream), zero past N
     float* NMX;   // -(row max) of the proposed rows: the replay's Symmetry stream
     float4* CLA;  // boxes of clearances 64.. (the first 64: registers, Own::cla0)
     uint64_t* NZ;  // pair words of clearances 64.. (the first 64 rows: registers, Own::nz0)
@@ -122,15 +128,21 @@ struct DeltaPtrs {
 
 // ---- per-object quantities --------------------------------------------------------------------
 
-__device__ __forceinline__ float4 obj_box(const DeltaPtrs& ch, int j) {
-    const ObjP p = ch.P[j];
-    return shape_box(ch.objs[j], p.xf, p.yf);
+__device__ __forceinline__ float4 obj_box(const DeltaPtrs& ch, int j) { return ch.BOX[j]; }
+
+// Object k's float pose {xf, yf, rotYf} (the .pad word is not set).
+__device__ __forceinline__ ObjP obj_pose(const DeltaPtrs& ch, int k) {
+    ObjP p;
+    p.xf = (float)ch.X[k];
+    p.yf = (float)ch.Y[k];
+    p.rotYf = ch.RYF[k];
+    p.pad = 0.0f;
+    return p;
 }
 
 __device__ __forceinline__ float4 cla_box(const DeltaPtrs& ch, int ci) {
     const RectShape& cs = ch.clrs[ci];
-    const ObjP p = ch.P[cs.pad];
-    return shape_box(cs, p.xf, p.yf);
+    return shape_box(cs, (float)ch.X[cs.pad], (float)ch.Y[cs.pad]);
 }
 
 // Clearance ci's box: its owner lane's register (ci < 64) or LDS. `own`: this lane owns ci.
@@ -147,17 +159,15 @@ __device__ __forceinline__ void cla_put(const DeltaPtrs& ch, Own<S>& o, int ci, 
 // SurfaceAreaCosts entry e (Kernel.cu:453-480): clearance e's box at cfg[e] (the reference's
 // quirk, :456) for e < C, then object e - C's off-limits box.
 __device__ __forceinline__ float4 sa_entry(const DeltaPtrs& ch, int c, int e) {
-    if (e < c) {
-        const ObjP p = ch.P[e];
-        return comp_overlaps(*ch.rm, shape_box(ch.clrs[e], p.xf, p.yf));
-    }
+    if (e < c)
+        return comp_overlaps(*ch.rm, shape_box(ch.clrs[e], (float)ch.X[e], (float)ch.Y[e]));
     return comp_overlaps(*ch.rm, obj_box(ch, e - c));
 }
 
 // FocalPointCosts term of object i, Kernel.cu:271,277 with phi() of :185-188.
-__device__ __forceinline__ float focal_cos(const DevRoom& rm, ObjP p) {
-    const float at = atan2_f32(rm.fyf - p.yf, rm.fxf - p.xf);
-    const float b = at - p.rotYf;
+__device__ __forceinline__ float focal_cos(const DevRoom& rm, float xf, float yf, float ryf) {
+    const float at = atan2_f32(rm.fyf - yf, rm.fxf - xf);
+    const float b = at - ryf;
     const float ph = (float)((double)b + kHalfPI);
     return cos_f32(ph);
 }
@@ -203,7 +213,8 @@ __device__ __forceinline__ RowMax scan_row(const DeltaPtrs& ch, const Own<S>& o,
     for (int q = 0; q < S; ++q) {
         const int j = q * L + r;
         if (j < n) {
-            const float v = sym_val_fast(*reinterpret_cast<const float4*>(&ch.P[j]), rx, ry, rr);
+            const float v = sym_val_fast(make_float4(o.xf[q], o.yf[q], (float)o.ry[q], 0.0f), rx,
+                                         ry, rr);
             t2 = __builtin_amdgcn_fmed3f(t1, t2, v);
             const bool up = v > t1;
             t1 = up ? v : t1;
@@ -213,8 +224,8 @@ __device__ __forceinline__ RowMax scan_row(const DeltaPtrs& ch, const Own<S>& o,
     const SymLead ld = group_sym_lead<L>(t1, t2, tj, r, 0, rr);
     RowMax out;
     if (!exact_mode && ld.clear) {
-        const ObjP q = ch.P[ld.j];
-        const float e = sym_val_exact(q.xf, q.yf, obj_ry<S>(o, ld.j), rx, ry, (double)rr);
+        const float e = sym_val_exact((float)ch.X[ld.j], (float)ch.Y[ld.j], obj_ry<S>(o, ld.j),
+                                      rx, ry, (double)rr);
         out.mx = fmaxf(0.0f, e);
         out.arg = e > 0.0f ? ld.j : -1;
         return out;
@@ -227,10 +238,10 @@ __device__ __forceinline__ RowMax scan_row(const DeltaPtrs& ch, const Own<S>& o,
     for (int q = 0; q < S; ++q) {
         const int j = q * L + r;
         if (j < n) {
-            const ObjP p = ch.P[j];
-            const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
+            const float v = sym_val_fast(make_float4(o.xf[q], o.yf[q], (float)o.ry[q], 0.0f), rx,
+                                         ry, rr);
             if (!(v < ld.m - thr)) {
-                const float e = sym_val_exact(p.xf, p.yf, o.ry[q], rx, ry, (double)rr);
+                const float e = sym_val_exact(o.xf[q], o.yf[q], o.ry[q], rx, ry, (double)rr);
                 if (e > bv) {
                     bv = e;
                     bj = j;
@@ -250,8 +261,8 @@ template <int S>
 __device__ __forceinline__ void symmetry_delta(const DeltaPtrs& ch, Own<S>& o, int n, int ka, int kb,
                                bool exact_mode, int r) {
     float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
-    if (ka >= 0) qa = *reinterpret_cast<const float4*>(&ch.P[ka]);
-    if (kb >= 0) qb = *reinterpret_cast<const float4*>(&ch.P[kb]);
+    if (ka >= 0) qa = make_float4((float)ch.X[ka], (float)ch.Y[ka], ch.RYF[ka], 0.0f);
+    if (kb >= 0) qb = make_float4((float)ch.X[kb], (float)ch.Y[kb], ch.RYF[kb], 0.0f);
     const double rya = obj_ry<S>(o, ka < 0 ? 0 : ka), ryb = obj_ry<S>(o, kb < 0 ? 0 : kb);
     unsigned pa = 0, pb = 0, resc = 0;
 #pragma unroll
@@ -304,8 +315,8 @@ __device__ __forceinline__ void symmetry_delta(const DeltaPtrs& ch, Own<S>& o, i
             const int i = tt * L + r;
             float rx, ry, rr;
             row_setup(ch, i, o.ry[tt], rx, ry, rr);
-            const ObjP q = ch.P[col];
-            const float e = sym_val_exact(q.xf, q.yf, ryc, rx, ry, (double)rr);
+            const float4 q = col == ka ? qa : qb;
+            const float e = sym_val_exact(q.x, q.y, ryc, rx, ry, (double)rr);
             const float cm = o.cmx[tt];
             const int ca = o.carg[tt];
             const float sm = o.pmx[tt];
@@ -424,7 +435,7 @@ __device__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
             const int q = __builtin_ctzll(pend) * L + r;
             pend &= pend - 1;
             double tpw, tang;
-            rel_terms(ch.relg[q], ch.P, tpw, tang);
+            rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
             ch.RPW[q] = -tpw;
             ch.RANG[q] = -tang;
         }
@@ -535,7 +546,7 @@ __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, con
             bt.ny += ty;
             bt.anx += fabsf(tx);
             bt.any += fabsf(ty);
-            const float w = ch.P[i].pad;
+            const float w = ch.CPH[i];
             bt.fp += w;
             bt.afp += fabsf(w);
             bt.sym -= o.pmx[t];
@@ -558,27 +569,28 @@ template <int S>
 __device__ __forceinline__ DBackup read_obj(const DeltaPtrs& ch, const Own<S>& o, int k) {
     DBackup b;
     b.k = k;
-    b.w = ch.P[k].pad;
+    b.w = ch.CPH[k];
     b.x = ch.X[k];
     b.y = ch.Y[k];
     b.ry = obj_ry<S>(o, k);
     return b;
 }
 
-// New pose of object k (its FocalPoint term is refreshed separately): LDS by `writer`, rotY in
-// the owner lane's registers.
+// New pose of object k (its FocalPoint term is refreshed separately): LDS (with its box) by
+// `writer`, the owner lane's registers.
 template <int S>
 __device__ __forceinline__ void write_pose(const DeltaPtrs& ch, Own<S>& o, int r, bool writer,
                                            int k, double x, double y, double ry) {
     if (writer) {
         ch.X[k] = x;
         ch.Y[k] = y;
-        float* p = &ch.P[k].xf;
-        p[0] = (float)x;
-        p[1] = (float)y;
-        p[2] = (float)ry;
+        ch.BOX[k] = shape_box(ch.objs[k], (float)x, (float)y);
+        ch.RYF[k] = (float)ry;
     }
-    slot_put<S>(o.ry, k >> 6, ry, r == (k & 63));
+    const bool own = r == (k & 63);
+    slot_put<S>(o.ry, k >> 6, ry, own);
+    slot_put<S>(o.xf, k >> 6, (float)x, own);
+    slot_put<S>(o.yf, k >> 6, (float)y, own);
 }
 
 template <int S, class Rng>
@@ -701,7 +713,7 @@ __device__ __forceinline__ void save_best_delta(const DeltaPtrs& ch, const Own<S
 // 5 SurfaceArea (float, float); 6/7 PairWise and PairWiseAngle (double, double). Each step is
 // rn_d(acc + v) with v the (negated where the reference subtracts) term, rounded on to float
 // for the float accumulators. Every lane reads three streams -- multiplier m, double d, float f
-// (the FocalPoint terms sit in the pose records, every fourth float) -- and adds v = m * d + f;
+// -- and adds v = m * d + f;
 // the streams a sum does not use are ones or zeros, and each sequence is zero past its end, so
 // v is the reference's term exactly.
 // Sums list terms [from, to) of `fs` (the float list of lane k = 4 or 5) into the float
@@ -738,14 +750,12 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     const float* ms = ch.ONES;
     const double* ds = ch.ZERO;
     const float* fs = reinterpret_cast<const float*>(ch.ZERO);
-    int fst = 1;      // this lane's float-stream stride
     int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
         ds = k == 0 ? ch.X : ch.Y;
     } else if (k == 2) {
-        fs = &ch.P[0].pad;
-        fst = 4;
+        fs = ch.CPH;
     } else if (k == 3) {
         fs = ch.NMX;
     } else if (k == 4) {
@@ -765,14 +775,13 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
         const bool in = l0 < lim;
         const float* msl = in ? ms : ch.ONES;
         const double* dsl = in ? ds : ch.ZERO;
-        const float* fsl = in ? fs + l0 * fst : reinterpret_cast<const float*>(ch.ZERO) + l0;
-        const int st = in ? fst : 1;
+        const float* fsl = in ? fs : reinterpret_cast<const float*>(ch.ZERO);
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             // one rounding either way: rn(m * d) where f = 0 (VisualBalance: m = area) and
             // rn(d + f) where m = 1 (every other sum), so the fused form is the two-step one
-            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fsl[u * st]);
+            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fsl[l0 + u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];
@@ -901,7 +910,9 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     ch.ZERO = reinterpret_cast<const double*>(lds + lay.h_zero);
     ch.X = reinterpret_cast<double*>(base + lay.X);
     ch.Y = reinterpret_cast<double*>(base + lay.Y);
-    ch.P = reinterpret_cast<ObjP*>(base + lay.P);
+    ch.BOX = reinterpret_cast<float4*>(base + lay.BOX);
+    ch.RYF = reinterpret_cast<float*>(base + lay.RYF);
+    ch.CPH = reinterpret_cast<float*>(base + lay.CPH);
     ch.NMX = reinterpret_cast<float*>(base + lay.NMX);
     const int np = lay.NP;
     ch.CLA = reinterpret_cast<float4*>(base + lay.CLA);
@@ -930,25 +941,31 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
 #pragma unroll
     for (int t = 0; t < S; ++t) {
         o.ry[t] = 0.0;
+        o.xf[t] = o.yf[t] = 0.0f;
         o.cmx[t] = o.pmx[t] = 0.0f;
         o.carg[t] = o.parg[t] = -1;
         o.nz0[t] = 0ull;
         o.cla0 = make_float4(0.f, 0.f, 0.f, 0.f);
         const int i = t * L + r;
-        if (i < n) o.ry[t] = src[F_RY * n + i];
+        if (i < n) {
+            o.ry[t] = src[F_RY * n + i];
+            o.xf[t] = (float)src[F_X * n + i];
+            o.yf[t] = (float)src[F_Y * n + i];
+        }
     }
     for (int i = r; i < np; i += L) {
         double x = 0.0, y = 0.0;
-        ObjP p;
-        p.xf = p.yf = p.rotYf = p.pad = 0.0f;
+        float ryf = 0.0f;
+        float4 box = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n) {
             x = src[F_X * n + i];
             y = src[F_Y * n + i];
-            p.xf = (float)x;
-            p.yf = (float)y;
-            p.rotYf = (float)src[F_RY * n + i];
+            ryf = (float)src[F_RY * n + i];
+            box = shape_box(objs_l[i], (float)x, (float)y);
         }
-        ch.P[i] = p;
+        ch.BOX[i] = box;
+        ch.RYF[i] = ryf;
+        ch.CPH[i] = 0.0f;
         ch.X[i] = x;
         ch.Y[i] = y;
         ch.NMX[i] = 0.0f;
@@ -964,7 +981,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
     for (int t = 0; t < S; ++t) {
         const int i = t * L + r;
         if (i < n) {
-            ch.P[i].pad = -focal_cos(*rm_l, ch.P[i]);
+            ch.CPH[i] = -focal_cos(*rm_l, o.xf[t], o.yf[t], (float)o.ry[t]);
             wild += wild_pose(ch.X[i], ch.Y[i], o.ry[t]) ? 1 : 0;
         }
     }
@@ -984,9 +1001,10 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
 
     const ChainMeta m0 = a.meta[chain];
     const bool writer = r == 0;
+    float cur[8];  // resultCosts of the current configuration (wave-uniform: scalar registers)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = uniform_f(m0.costs[k]);
     float cur_total = m0.costs[0];
-    if (writer)
-        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
     typename RngOf<XW, L>::type rng;
     rng_load(rng, a, chain, m0);
     uint64_t accepted = m0.accepted;
@@ -1012,9 +1030,9 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         if (r < 2) {
             const int k = r == 0 ? ka : kb;
             if (k >= 0) {
-                const ObjP p = ch.P[k];
-                ch.P[k].pad = -focal_cos(*rm_l, p);
-                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.objs[k], p.xf, p.yf))));
+                const ObjP p = obj_pose(ch, k);
+                ch.CPH[k] = -focal_cos(*rm_l, p.xf, p.yf, p.rotYf);
+                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, ch.BOX[k])));
                 if (k < c)
                     sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrs[k], p.xf, p.yf))));
                 const DBackup& ob = ch.aux->b[r];
@@ -1105,17 +1123,16 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             o.cmx = o.pmx;
             o.carg = o.parg;
             wild_cnt = wild_star;
-            if (writer) {
-                for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
-                commit_swap_zrr(ch, n);
-            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = uniform_f(sc[k]);
+            if (writer) commit_swap_zrr(ch, n);
             wave_sync();
         } else {
             const int nb = ch.aux->nb;
             for (int q = nb - 1; q >= 0; --q) {
                 const DBackup b = ch.aux->b[q];
                 write_pose<S>(ch, o, r, writer, b.k, b.x, b.y, b.ry);
-                if (writer) ch.P[b.k].pad = b.w;
+                if (writer) ch.CPH[b.k] = b.w;
             }
             for (int w = r; w < ch.SW; w += L) ch.SAM[w] = ch.SAMB[w];
             wave_sync();
@@ -1137,7 +1154,7 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         m.bm_has = rng.bm_has;
         m.bm_val = rng.bm_val;
         rng_save(rng, a, chain);
-        for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
+        for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
         m.best_total = best_total;
         m.rung = m0.rung;
         a.meta[chain] = m;

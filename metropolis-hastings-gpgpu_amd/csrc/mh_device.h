@@ -187,8 +187,9 @@ struct DeltaLds {
     int NR;         // relationship stream length round4(max(R, 1))
     int DL;         // dense replay length max(NP, NR)
     int X, Y;       // double[NP] (zero past N)
-    int P;          // float4[NP] {xf, yf, rotYf, -cos(phi)} (zero past N): the FocalPoint terms
-                    // are every fourth float of it
+    int BOX;        // float4[NP] object off-limits boxes at the current poses (zero past N)
+    int RYF;        // float[NP] (float)rotY
+    int CPH;        // float[NP] -cos(phi), the FocalPoint terms (zero past N)
     int NMX;        // float[NP] -(row max) of the proposed symmetry rows (the replay's stream)
     int CLA;        // float4[C - 64] boxes of clearances 64.. at their source objects (the first
                     // 64 live in the owner lanes' registers)
@@ -204,7 +205,7 @@ struct DeltaLds {
     int stride;     // bytes per chain
 };
 
-constexpr int kDeltaAuxBytes = 112;  // mh_delta.hip DeltaAux: two undo records, the current costs
+constexpr int kDeltaAuxBytes = 80;  // mh_delta.hip DeltaAux: two undo records, the swap
 
 inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     DeltaLds l;
@@ -233,7 +234,9 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     int o = 0;
     l.X = o;    o += 8 * np;
     l.Y = o;    o += 8 * np;
-    l.P = o;    o += 16 * np;
+    l.BOX = o;  o += 16 * np;
+    l.RYF = o;  o += 4 * np;
+    l.CPH = o;  o += 4 * np;
     l.NMX = o;  o += round16(4 * np);
     l.CLA = o;  o += 16 * (c > 64 ? c - 64 : 1);  // clearances 64.. (the first 64: registers)
     l.NZ = o;   o += 8 * l.W * (c > 64 ? c - 64 : 1);  // rows 64..: the first 64 are registers
