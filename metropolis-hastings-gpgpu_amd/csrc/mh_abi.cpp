@@ -369,6 +369,12 @@ struct mh_session {
     resultCosts* d_costs = nullptr;
     mh_summary* d_summary = nullptr;
 
+    static float bound_slack() {
+        const char* e = getenv("MH_BOUND_SLACK");
+        const float v = e ? (float)atof(e) : 1.0f;
+        return v >= 1.0f ? v : 1.0f;  // (a narrower allowance would not be a bound)
+    }
+
     mh::LaunchArgs args() const {
         mh::LaunchArgs a{};
         a.rm = room.rm;
@@ -390,6 +396,7 @@ struct mh_session {
         a.xw = d_xw;
         a.n_temps = n_temps;
         a.ladder = d_ladder;
+        a.bound_slack = bound_slack();
         a.lay = geo.lay;
         a.dlay = geo.dlay;
         return a;

@@ -61,8 +61,9 @@ struct ChainAux {
     int swap_a, swap_b;  // a swap proposal's objects (-1: none); z/rotX/rotZ swap in HBM on accept
     float cur[8]; // resultCosts of the current configuration
 #if MH_STAMPS
-    unsigned long long cyc[10];  // diagnostic: cycles per phase (writer lane); [8] steps that
-                                 // evaluated the rejection bound, [9] steps it rejected
+    unsigned long long cyc[12];  // diagnostic: cycles per phase (writer lane); [8] steps that
+                                 // evaluated the bound, [9] steps it rejected, [10] steps it
+                                 // accepted, [11] exact evaluations of the current configuration
 #endif
 };
 static_assert(sizeof(ChainAux) <= kChainAuxBytes, "ChainAux");
@@ -242,15 +243,18 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
 // differs from the evaluated one only in objects ka and kb (-1: none), and only the rows and
 // columns those objects touch are re-evaluated.
 // FAST (steps without best-of-chain tracking, one chain per wavefront): before any ordered sum
-// is built, the proposal's total is bounded from lane-parallel sums (certain_reject) and, when
-// the bound already decides Accept's rejection for the drawn uniform `u_acc`, the function
-// returns with *fast_reject set and `out` unset; otherwise it goes on to the exact costs.
+// is built, the proposal's total is bounded from lane-parallel sums (bound_decide, against the
+// current total's interval `cur`) and, when the bound already decides Accept for the drawn
+// uniform `u_acc`, the function returns with *fast set to BOUND_REJECT or BOUND_ACCEPT, the
+// proposal's interval in *star_iv and `out` unset (the symmetry rows and Clearance pairs are
+// set: they come before the bound); otherwise it goes on to the exact costs.
 template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false>
 __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPose<NPL>& op,
                            int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
-                           float cur_total = 0.0f, bool* fast_reject = nullptr) {
+                           CostIv cur = CostIv{0.0f, 0.0f}, int* fast = nullptr,
+                           CostIv* star_iv = nullptr) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
     const DevRoom& rm = *ch.rm;
@@ -672,16 +676,18 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
             bt.ang = -(float)rang[0];
             bt.aang = fabsf(bt.ang);
             bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
-            const bool rej = certain_reject(rm, n, c, rm.r, cl_total, bt, u_acc, cur_total);
+            const int d = bound_decide(rm, n, c, rm.r, cl_total, bt, u_acc, cur, *star_iv,
+                                       a.bound_slack);
             if (r == 0) MH_PHASE(ch, 4, t0);
 #if MH_STAMPS
             if (r == 0) {
                 ch.aux->cyc[8] += 1;
-                ch.aux->cyc[9] += rej ? 1 : 0;
+                ch.aux->cyc[9] += d == BOUND_REJECT ? 1 : 0;
+                ch.aux->cyc[10] += d == BOUND_ACCEPT ? 1 : 0;
             }
 #endif
-            if (rej) {
-                *fast_reject = true;
+            if (d != BOUND_OPEN) {
+                *fast = d;
                 return;
             }
         }
@@ -1254,6 +1260,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         if (writer)
             for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
         float cur_total = m0.costs[0];
+        bool cur_exact = true;  // (plain steps: false after a proposal accepted on the bound)
+        CostIv cur_iv{cur_total, cur_total};
         Rng rng;
         rng_load(rng, a, chain, m0);
         uint64_t accepted = m0.accepted;
@@ -1265,7 +1273,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         eval_costs<L, NPL, false, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, cl, cl);
 #if MH_STAMPS
         if (writer)
-            for (int k = 0; k < 10; ++k) ch.aux->cyc[k] = 0;
+            for (int k = 0; k < 12; ++k) ch.aux->cyc[k] = 0;
 #endif
 #pragma clang loop unroll(disable)
         for (int it = 0; it < a.iterations; ++it) {
@@ -1281,13 +1289,54 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             // Steps of plain chains, one per wavefront: Accept's uniform (the next draw after the
             // proposal's, Kernel.cu:710) is drawn first, so a proposal the rejection bound
             // already rejects skips the exact sums (eval_costs FAST).
+            // A proposal the bound accepts is taken without its exact costs: the current total is
+            // then known as an interval (cur_iv) until a step needs it exactly (below).
             constexpr bool FASTK = !TRACK && NPL == 1 && L == 64 && !(MH_ABLATE & 4);
-            bool fast_rej = false;
+            int fast = BOUND_OPEN;
+            CostIv star_iv{0.0f, 0.0f};
             float u_acc = 0.0f;
             if constexpr (FASTK) u_acc = rng.uniform();
             eval_costs<L, NPL, false, true, FASTK>(a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y,
-                                                    cls, cl, u_acc, cur_total, &fast_rej);
+                                                    cls, cl, u_acc, cur_iv, &fast, &star_iv);
             MH_STAMP(ts);
+            if constexpr (FASTK) {
+                if (fast == BOUND_OPEN && !cur_exact) {
+                    // The decision needs the current configuration's exact costs: undo the
+                    // proposal, evaluate the current configuration incrementally from the
+                    // proposal's state (the same two objects differ), and keep the proposal's
+                    // poses in the backup slots so that restore() re-applies them.
+                    const int nb = ch.aux->nb;
+                    const int k0 = nb > 0 ? ch.aux->b[0].k : 0, k1 = nb > 1 ? ch.aux->b[1].k : 0;
+                    const Backup s0 = read_obj<L, NPL>(op, k0, gbase);
+                    const Backup s1 = read_obj<L, NPL>(op, k1, gbase);
+                    restore<L, NPL>(ch, op, r, writer);
+                    wave_sync();
+                    float cx[8];
+                    SymRows<NPL> sx;
+                    ClPairs clx;
+                    eval_costs<L, NPL, false, true>(a, ch, op, r, gbase, cx, sx, ss, kk.x, kk.y, clx,
+                                                    cls);
+                    if (writer) {
+                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = cx[k];
+                        if (nb > 0) ch.aux->b[0] = s0;
+                        if (nb > 1) ch.aux->b[1] = s1;
+                    }
+#if MH_STAMPS
+                    if (writer) ch.aux->cyc[11] += 1;
+#endif
+                    cur_total = uniform_f(cx[0]);
+                    cur_exact = true;
+                    cur_iv = CostIv{cur_total, cur_total};
+                    wave_sync();
+                    if (u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total))) {
+                        restore<L, NPL>(ch, op, r, writer);  // the proposal again
+                        fast = BOUND_ACCEPT + 1;  // accepted with exact costs (below)
+                    } else {
+                        fast = BOUND_REJECT + 16;  // rejected, already undone
+                    }
+                    wave_sync();
+                }
+            }
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if constexpr (TRACK) {
                 if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
@@ -1296,29 +1345,54 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 }
             }
             bool acc;
+            bool exact = true;  // accepted with its exact costs
             if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
-            else if constexpr (FASTK)
-                acc = !fast_rej &&
-                      u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
-            else acc = accept(rng, sc[0], cur_total);
+            else if constexpr (FASTK) {
+                if (fast == BOUND_OPEN)
+                    acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
+                else
+                    acc = fast == BOUND_ACCEPT || fast == BOUND_ACCEPT + 1;
+                exact = fast != BOUND_ACCEPT;
+            } else acc = accept(rng, sc[0], cur_total);
             if (acc) {
-                cur_total = sc[0];
                 sym = ss;
                 cl = cls;
                 ++accepted;
+                if (exact) {
+                    cur_total = sc[0];
+                    if constexpr (FASTK) {
+                        cur_exact = true;
+                        cur_iv = CostIv{cur_total, cur_total};
+                    }
+                } else if constexpr (FASTK) {
+                    cur_exact = false;
+                    cur_iv = star_iv;
+                }
                 if (writer) {
-                    for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
+                    if (exact)
+                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
                     commit_swap_zrr(ch, n);
                 }
-            } else {
+            } else if (fast != BOUND_REJECT + 16) {
                 restore<L, NPL>(ch, op, r, writer);
             }
             wave_sync();
             if (writer) MH_PHASE(ch, 7, ts);
         }
+        if (!cur_exact) {
+            // The exact costs of the final configuration: an incremental evaluation with no
+            // object changed recomputes only the ordered sums.
+            float cx[8];
+            SymRows<NPL> sx;
+            ClPairs clx;
+            eval_costs<L, NPL, false, true>(a, ch, op, r, gbase, cx, sx, sym, -1, -1, clx, cl);
+            if (writer)
+                for (int k = 0; k < 8; ++k) ch.aux->cur[k] = cx[k];
+            wave_sync();
+        }
 #if MH_STAMPS
         if (writer)
-            for (int k = 0; k < 10; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
+            for (int k = 0; k < 12; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
 #endif
         if (writer) {
             ChainMeta m;
@@ -1690,7 +1764,7 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 10) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 12) ==
                    hipSuccess ? 0 : -1;
 }
 #endif

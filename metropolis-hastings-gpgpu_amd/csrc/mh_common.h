@@ -702,21 +702,44 @@ __device__ __forceinline__ void wave_fsum8(const float (&v)[8], float (&s)[8]) {
     s[7] = __int_as_float(__builtin_amdgcn_readlane(di, 49));
 }
 
-// Whether Accept certainly rejects this proposal, for a chain that owns the wavefront. n
-// objects, c clearances, nrel relationships, ncl non-zero Clearance terms. The arithmetic after
-// the lane sums is fp32 on wave-uniform values; every intermediate has at most ~30 roundings
-// on quantities no larger than M (below), so 64 U M covers them.
-__device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
-                                               const BoundTerms& bt, float u, float cur) {
+// A wave-uniform float, in a scalar register.
+__device__ __forceinline__ float uniform_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// An interval of fp32 totals (a chain's current total is an exact value, lo == hi, or, after a
+// proposal accepted on the bound alone, the bound's interval around the exact total).
+struct CostIv {
+    float lo, hi;
+};
+
+enum { BOUND_OPEN = 0, BOUND_REJECT = 1, BOUND_ACCEPT = 2 };
+
+// Whether Accept's decision for this proposal is already certain, for a chain that owns the
+// wavefront: BOUND_REJECT / BOUND_ACCEPT, or BOUND_OPEN (the exact costs are needed). n objects,
+// c clearances, nrel relationships, ncl non-zero Clearance terms; `cur` holds the current
+// total. The arithmetic after the lane sums is fp32 on wave-uniform values; every intermediate
+// has at most ~30 roundings on quantities no larger than M (below), so 64 U M covers them, and
+// the proposal's exact total lies in t +- 1.25 e. `star` receives an interval around it that
+// also absorbs the rounding of its own ends (e >= 64 U |t|, so 0.25 e does).
+__device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                            const BoundTerms& bt, float u, CostIv cur,
+                                            CostIv& star, float slack = 1.0f) {
     constexpr float U = 0x1p-24f;
     const float kf = (float)bt.k;
     const float lfp = rm.w_fp * bt.fp, lsym = rm.w_sym * bt.sym, lcl = rm.w_cl * bt.cl,
                 lsa = rm.w_sa * bt.sa;
     const float lin = (lfp + lsym) + (lcl + lsa);
     const float afp = fabsf(rm.w_fp) * bt.afp;
-    const float elin = (2.0f * n + 26.0f + kf) * U * (afp + fabsf(lsym)) +
-                       (2.0f * ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
-                       (8.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
+    // A sequential sum of m terms in a float accumulator is within (m - 1) U (1 + m U) sum |t|
+    // of the exact sum (one rounding to nearest per add); in a double accumulator within
+    // m 2^-53 (1 + m 2^-53) sum |t|. Our estimate: terms rounded to float once, k pre-summed per
+    // lane, a six-level tree: (k + 7) U sum |t|. "26" covers both second-order parts for
+    // m < 2^20. FocalPoint accumulates in double, Symmetry, Clearance and SurfaceArea in float.
+    const float eacc = 0x1p-29f * (float)(n + nrel);  // (double accumulators, in units of U)
+    const float elin = (26.0f + kf + eacc) * U * afp + (n + 26.0f + kf) * U * fabsf(lsym) +
+                       (ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
+                       (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
                        12.0f * U * (afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
     // sums of |t| for VisualBalance: one sum of |area x| + |area y| bounds both coordinates'
     const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin, bt.anx + bt.any, bt.aang};
@@ -729,7 +752,7 @@ __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, 
                 a_ang = fmaxf(fabsf(s_ang), sum[7]);
     // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
     const float id = fabsf(rm.inv_denom);
-    const float cv = (2.0f * n + 26.0f + kf) * U;
+    const float cv = (n + 26.0f + kf) * U;  // (float accumulators, Kernel.cu:200-201)
     const float enx = cv * a_nx * id, eny = cv * a_ny * id;
     const float ad = s_nx * rm.inv_denom, bd = s_ny * rm.inv_denom;
     const float da = enx + 3.0f * U * (fabsf(ad) + enx), db = eny + 3.0f * U * (fabsf(bd) + eny);
@@ -740,7 +763,7 @@ __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, 
     const float o2 = rm.w_vb * vb;
     const float e2 = fabsf(rm.w_vb) * (dvb + 3.0f * U * (fabsf(vb) + dvb));
     // PairWise x PairWiseAngle (Kernel.cu:518)
-    const float cr = (2.0f * nrel + 26.0f + kf) * U;
+    const float cr = (26.0f + kf + eacc) * U;  // (double accumulators, :222, :249-253)
     const float epw = cr * fabsf(s_pw), eang = cr * a_ang;
     const float pa = s_pw * s_ang;
     const float dpa = fabsf(s_pw) * eang + fabsf(s_ang) * epw + epw * eang;
@@ -748,16 +771,33 @@ __device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, 
     const float e1 = fabsf(rm.w_pw) * (dpa + 3.0f * U * (fabsf(pa) + dpa));
     // total (Kernel.cu:547) and its upper end
     const float t = (o1 + o2) + s_lin;
-    const float m = fabsf(o1) + fabsf(o2) + fabsf(s_lin) + e1 + e2 + s_elin + fabsf(cur) +
+    const float acur = fmaxf(fabsf(cur.lo), fabsf(cur.hi));
+    const float m = fabsf(o1) + fabsf(o2) + fabsf(s_lin) + e1 + e2 + s_elin + acur +
                     fabsf(vb) + fabsf(fx) + fabsf(fy) + fabsf(rm.w_pw) * fabsf(pa);
-    const float e = e1 + e2 + s_elin + 12.0f * U * (fabsf(o1) + e1 + fabsf(o2) + e2) + 64.0f * U * m;
-    const float x = (float)kBeta * ((t + 1.25f * e) - cur);
+    const float e = slack * (e1 + e2 + s_elin + 12.0f * U * (fabsf(o1) + e1 + fabsf(o2) + e2) +
+                             64.0f * U * m);
+    const float x = (float)kBeta * ((t + 1.25f * e) - cur.lo);   // beta (star - cur), upper end
+    const float xl = (float)kBeta * ((t - 1.25f * e) - cur.hi);  // and lower end
     // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
     const float lu = __logf(u);
-    // x <= lu - 1e-4 (the uniform compare NaN-false: an invalid bound is never certain); the
-    // chain's first lane decides, so the decision is wave-uniform by construction
+    // Reject: x <= lu - 1e-4 (the compares are NaN-false: an invalid bound is never certain).
+    // Accept: accept_threshold is 1 for beta (star - cur) >= 0, so u < 1 decides; otherwise
+    // exp(beta (star - cur)) (> exp(-24)) exceeds u when log(u) < xl - 1e-4.
     const bool rej = x <= lu - 1e-4f && x > -1e30f;
-    return __builtin_amdgcn_readfirstlane(rej ? 1 : 0) != 0;
+    const bool acc = (xl >= 0.0f && u < 1.0f) || (xl > -23.9f && lu < xl - 1e-4f);
+    star.lo = t - 1.5f * e;
+    star.hi = t + 1.5f * e;
+    // the chain's first lane decides, so the decision is wave-uniform by construction
+    return __builtin_amdgcn_readfirstlane(rej ? BOUND_REJECT : (acc ? BOUND_ACCEPT : BOUND_OPEN));
+}
+
+// Whether Accept certainly rejects this proposal (bound_decide with an exact current total).
+__device__ __forceinline__ bool certain_reject(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                               const BoundTerms& bt, float u, float cur,
+                                               float slack = 1.0f) {
+    CostIv star;
+    return bound_decide(rm, n, c, nrel, ncl, bt, u, CostIv{cur, cur}, star, slack) ==
+           BOUND_REJECT;
 }
 
 // Exact row maxima of the symmetry rows this lane owns (rows m * L + r), with the column that

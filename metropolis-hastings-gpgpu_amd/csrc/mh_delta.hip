@@ -79,10 +79,6 @@ __device__ __forceinline__ void slot_put(V& v, int m, T x, bool pred) {
     for (int q = 0; q < S; ++q) v[q] = (pred && q == m) ? x : v[q];
 }
 
-__device__ __forceinline__ float uniform_f(float v) {  // (v is wave-uniform)
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-
 // rotY of object k (wave-uniform k), from its owner lane.
 template <int S>
 __device__ __forceinline__ double obj_ry(const Own<S>& o, int k) {
@@ -1066,7 +1062,8 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             bt.cl = clsum;
             bt.kcl = kcl;
             bt.sa = sasum;
-            fast_rej = certain_reject(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_total);
+            fast_rej = certain_reject(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_total,
+                                      a.bound_slack);
         }
 #if MH_STAMPS > 1
         if (r == 0) {

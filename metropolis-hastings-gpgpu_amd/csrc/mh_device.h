@@ -130,7 +130,7 @@ __device__ __forceinline__ void save_best(const Ptrs& ch, double* dst, int n, in
 
 // Per-chain scalars of the full-evaluation kernel (mh_chain.hip ChainAux), bytes.
 #if defined(MH_STAMPS) && MH_STAMPS
-constexpr int kChainAuxBytes = 192;
+constexpr int kChainAuxBytes = 224;
 #else
 constexpr int kChainAuxBytes = 128;
 #endif

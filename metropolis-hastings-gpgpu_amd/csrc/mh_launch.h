@@ -36,6 +36,8 @@ struct LaunchArgs {
     int n_temps;             // parallel tempering replicas per group (1 = off)
     const double* ladder;    // [n_temps] inverse temperatures (n_temps > 1)
     unsigned int* xw;        // [n_chains][6] XORWOW states {d, x0..x4} (rng == RNG_CURAND_XORWOW)
+    float bound_slack;       // diagnostic: widens the step bound's error allowance ($MH_BOUND_SLACK,
+                             // default 1; the tests use it to send many steps down the exact paths)
     ChainLds lay;
     DeltaLds dlay;           // incremental step kernel (mh_delta.hip)
 };

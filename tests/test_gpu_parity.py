@@ -628,3 +628,36 @@ def test_stacked_objects_symmetry_ties(mh, orc, hiplib, monkeypatch, step, n, ch
         pts, costs = s.download()
     ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
     check_chains(f"{step} stacked N={n}", pts, costs, ref_pts, ref_costs)
+
+
+@pytest.mark.parametrize("step", ["full", "incremental"])
+@pytest.mark.parametrize("slack", ["1", "4", "64", "1e6"])
+@pytest.mark.parametrize("kind,n,chains,steps", [
+    ("syn", 64, 64, 1200),   # config 3's room; two launches (the lazy costs cross a launch end)
+    ("main", 32, 64, 600),
+    ("wrap", 24, 64, 500),
+    ("syn", 9, 64, 500),
+])
+def test_bound_decision_paths(mh, orc, hiplib, monkeypatch, step, slack, kind, n, chains, steps):
+    """The step bound decides Accept without the exact costs where it can: a certain reject
+    (both step kernels) or, in the full-evaluation kernel, a certain accept that leaves the
+    current total known only as an interval; otherwise the exact costs are computed, the current
+    configuration's too when they are pending. $MH_BOUND_SLACK widens the bound's error
+    allowance (still a valid bound), which moves steps from the certain decisions to the exact
+    paths: every mix must give the oracle's chains."""
+    monkeypatch.setenv("MH_BOUND_SLACK", slack)
+    kind_ = _use_step(monkeypatch, step, n)
+    room = _room(mh, kind, n)
+    seed = 9100 + n
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel()[2] == kind_
+        s.run(steps)
+        cur = s.current_costs()
+        s.finalize()
+        pts, costs = s.download()
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
+    check_chains(f"slack {slack} {step} {kind} N={n}", pts, costs, ref_pts, ref_costs)
+    # the costs carried between launches are the exact ones (all but OffLimits, which the step
+    # path does not evaluate)
+    keep = [1, 2, 3, 4, 5, 7]
+    assert np.array_equal(cur[:, keep].view(np.uint32), costs[:, keep].view(np.uint32))

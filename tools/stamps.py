@@ -28,7 +28,7 @@ def main():
     with mh.Session(mh.synthetic_room(n), chains, seed=42) as s:
         s.run(iters)
         s.finalize()
-        s.summary()
+        acc_rate = s.summary().accepted / float(chains * iters)
         lanes, cpw, s_kind = s.step_kernel()
     out = (C.c_ulonglong * 14)()
     delta = hasattr(lib, "mh_debug_delta_cycles") and s_kind == "incremental"
@@ -40,13 +40,16 @@ def main():
         assert lib.mh_debug_phase_cycles(out) == 0
         names, per, unit = PHASES, chains * iters, "cycles/chain-step"
     tot = sum(out[:7] if delta else out[:8])  # (delta: [7] is a part of [5])
-    print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes} delta={delta}")
+    print(f"N={n} chains={chains} iters={iters} lanes/chain={lanes} delta={delta} "
+          f"acceptance={acc_rate:.4f}")
     for name, v in zip(names, out[:8]):
         print(f"  {name:18s} {100.0 * v / tot:6.2f}%   {v / per:10.1f} {unit}")
     if not delta and out[8]:
         steps = chains * iters
         print(f"  rejection bound evaluated on {out[8] / steps:.4f} of steps, certain reject on "
-              f"{out[9] / steps:.4f} ({out[9] / out[8]:.4f} of those evaluated)")
+              f"{out[9] / steps:.4f} ({out[9] / out[8]:.4f} of those evaluated), certain accept "
+              f"on {out[10] / steps:.4f}; exact costs of the current configuration recomputed on "
+              f"{out[11] / steps:.4f}")
     if delta and out[12]:  # counts (MH_STAMPS=2 builds): per step that reached the replay
         steps = chains * iters
         rep = max(1, out[12] - out[13])
