@@ -226,7 +226,7 @@ struct Geometry {
 };
 
 // Incremental step kernel geometry: one chain per wavefront; the workgroup size (chains per
-// workgroup, up to 12) that keeps the most chains resident per CU, as the runtime's occupancy
+// workgroup, up to 12, 8 above 128 objects) that keeps the most chains resident per CU, as the runtime's occupancy
 // calculator counts them (registers, LDS, waves), rounded down to whole waves per SIMD above
 // four; ties go to fewer waves per workgroup. The
 // kernel is latency-bound, so resident chains are its throughput (measured at N = 256: 1 to 5
@@ -242,7 +242,7 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     int best_chains = -1;
     g.dL = 64;
     g.dwaves = 0;
-    for (int w = 1; w <= 12; ++w) {  // (the kernel's launch bound: 768 threads)
+    for (int w = 1; w <= mh::delta_max_waves(n); ++w) {  // (the kernel's launch bound)
         if (want_w && w != want_w) continue;
         const size_t b = mh::delta_lds_bytes(g.dlay, w);
         if (b > (size_t)max_lds) continue;

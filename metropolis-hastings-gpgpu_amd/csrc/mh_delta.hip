@@ -845,13 +845,63 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     out[0] = t;
 }
 
+// Chains (waves) per workgroup the kernel is built for: rooms of more than 128 objects are held
+// by LDS to at most two chains per SIMD, so a bound of eight lets the allocator use up to 256
+// VGPRs (twelve would cap it at 168 and spill).
+constexpr int delta_max_waves_s(int S) { return S >= 4 ? 8 : 12; }
+
+// The exact costs of the configuration the caches hold, with symmetry rows `mx` (the proposal's
+// o.pmx or the current o.cmx), from the Clearance / SurfaceArea lists just built (counts cnt_cl,
+// cnt_sa): zero past each list's end, the Symmetry stream, the replay.
+template <int S>
+__device__ __forceinline__ void replay_config(const DeltaPtrs& ch, const typename Own<S>::fvec& mx,
+                                              const Own<S>& o, int n, int cnt_cl, int cnt_sa,
+                                              int r, float out[8],
+                                              unsigned long long* dense = nullptr) {
+    // zero past each list's end: to NP for the dense walk, to round4 for the list walk
+    const int zcl = max(ch.NP, (min(cnt_cl, ch.cap_cl) + 3) & ~3);
+    const int zsa = (min(cnt_sa, ch.cap_sa) + 3) & ~3;  // (lane 5's dense stream ends there)
+    for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) ch.LCL[l] = 0.0f;
+    for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) ch.LSA[l] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+        const int i = t * L + r;
+        if (i < n) ch.NMX[i] = -mx[t];
+    }
+    wave_sync();
+    replay<S>(ch, o, n, cnt_cl, cnt_sa, r, out, dense);
+}
+
+// Undoes the last proposal (objects ka, kb): the backed-up poses and FocalPoint terms, the
+// SurfaceArea bits (SAM <-> SAMB, so the proposal's bits stay in SAMB), the clearance boxes and
+// pair bits, the relationship terms.
+template <int S>
+__device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, int n, int c, int nr,
+                                              int ka, int kb, int r, bool writer) {
+    const int nb = ch.aux->nb;
+    for (int q = nb - 1; q >= 0; --q) {
+        const DBackup b = ch.aux->b[q];
+        write_pose<S>(ch, o, r, writer, b.k, b.x, b.y, b.ry);
+        if (writer) ch.CPH[b.k] = b.w;
+    }
+    for (int w = r; w < ch.SW; w += L) {
+        const uint32_t t = ch.SAM[w];
+        ch.SAM[w] = ch.SAMB[w];
+        ch.SAMB[w] = t;
+    }
+    wave_sync();
+    clearance_delta<S>(ch, o, n, c, ka, kb, r);
+    rels_delta(ch, nr, ka, kb, r);
+    wave_sync();
+}
+
 // ---- the kernel ---------------------------------------------------------------------------
 
 template <int S, bool XW, bool TRACK>
 // Up to 12 waves (chains) per workgroup: at large N one workgroup per CU holds every resident
 // chain, so the room tables staged in LDS are paid for once per CU (three waves per SIMD leave
 // the register allocator 168 registers).
-__global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
+__global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const DeltaLds& lay = a.dlay;
     const int n = a.rm.n, c = a.rm.c, nr = a.rm.r;
@@ -1001,6 +1051,11 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) cur[k] = uniform_f(m0.costs[k]);
     float cur_total = m0.costs[0];
+    // Plain chains take a proposal the rejection bound certainly accepts without its exact
+    // costs: the current total is then known as an interval (cur_iv, cur_exact false) until a
+    // step's decision needs it exactly, or the launch ends.
+    bool cur_exact = true;
+    CostIv cur_iv{cur_total, cur_total};
     typename RngOf<XW, L>::type rng;
     rng_load(rng, a, chain, m0);
     uint64_t accepted = m0.accepted;
@@ -1050,7 +1105,8 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         // drawn first. The Clearance and SurfaceArea lists are built with the bound's partial
         // sums, and a proposal the bound already rejects skips the replay.
         constexpr bool FASTD = !TRACK;
-        bool fast_rej = false;
+        int bd = BOUND_OPEN;
+        CostIv star_iv{0.0f, 0.0f};
         float u_acc = 0.0f;
         float clsum = 0.0f, sasum = 0.0f;
         int kcl = 0;
@@ -1062,29 +1118,21 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             bt.cl = clsum;
             bt.kcl = kcl;
             bt.sa = sasum;
-            fast_rej = certain_reject(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_total,
-                                      a.bound_slack);
+            // (not on a launch's last step: it ends with the current costs exact, through the
+            // exact pass below when they are not)
+            if (it + 1 < a.iterations)
+                bd = bound_decide(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_iv, star_iv,
+                                  a.bound_slack);
         }
 #if MH_STAMPS > 1
         if (r == 0) {
             atomicAdd(&g_delta_counts[4], 1ull);
-            atomicAdd(&g_delta_counts[5], (unsigned long long)(fast_rej ? 1 : 0));
+            atomicAdd(&g_delta_counts[5], (unsigned long long)(bd == BOUND_REJECT ? 1 : 0));
         }
 #endif
         float sc[8];
-        if (!fast_rej) {
-        // zero past each list's end: to NP for the dense walk, to round4 for the list walk
-        const int zcl = max(np, (min(cnt_cl, ch.cap_cl) + 3) & ~3);
-        const int zsa = (min(cnt_sa, ch.cap_sa) + 3) & ~3;  // (lane 5's dense stream ends there)
-        for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) ch.LCL[l] = 0.0f;
-        for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) ch.LSA[l] = 0.0f;
-#pragma unroll
-        for (int t = 0; t < S; ++t) {
-            const int i = t * L + r;
-            if (i < n) ch.NMX[i] = -o.pmx[t];
-        }
-        wave_sync();
-        DSTAMP(4);
+        bool rare = false;  // the exact pass of the current configuration ran (below)
+        if (bd == BOUND_OPEN) {
 #if MH_STAMPS > 1
         if (r == 0) {
             atomicAdd(&g_delta_counts[0], (unsigned long long)cnt_cl);
@@ -1093,11 +1141,47 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
             atomicAdd(&g_delta_counts[3], (unsigned long long)(cnt_sa > ch.cap_sa));
         }
 #endif
+        DSTAMP(4);
+        // Pass 0 replays the proposal's sums. When the current total is only an interval
+        // (FASTD, cur_exact false), pass 1 undoes the proposal and replays the current
+        // configuration's sums; one replay call site, so the rare pass adds no registers.
+        int lcl = cnt_cl, lsa = cnt_sa;
+#pragma clang loop unroll(disable)
+        for (int pass = 0;; ++pass) {
+            float ro[8];
+            typename Own<S>::fvec mx = o.pmx;
+            if (pass) mx = o.cmx;
 #if MH_STAMPS
-        replay<S>(ch, o, n, cnt_cl, cnt_sa, r, sc, &cyc[7]);
+            replay_config<S>(ch, mx, o, n, lcl, lsa, r, ro, &cyc[7]);
 #else
-        replay<S>(ch, o, n, cnt_cl, cnt_sa, r, sc);
+            replay_config<S>(ch, mx, o, n, lcl, lsa, r, ro);
 #endif
+            if (pass) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) cur[k] = uniform_f(ro[k]);
+                cur_total = cur[0];
+                cur_exact = true;
+                cur_iv = CostIv{cur_total, cur_total};
+                break;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sc[k] = uniform_f(ro[k]);  // (scalar registers)
+            if (!FASTD || cur_exact) break;
+            // The decision needs the current configuration's exact costs: undo the proposal.
+            // The undo records are swapped to its objects' poses and FocalPoint terms (and SAMB
+            // keeps its SurfaceArea bits), so a second undo_proposal() re-applies it.
+            const int nb = ch.aux->nb;
+            const DBackup p0 = read_obj<S>(ch, o, nb > 0 ? ch.aux->b[0].k : 0);
+            const DBackup p1 = read_obj<S>(ch, o, nb > 1 ? ch.aux->b[1].k : 0);
+            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer);
+            if (writer) {
+                if (nb > 0) ch.aux->b[0] = p0;
+                if (nb > 1) ch.aux->b[1] = p1;
+            }
+            lcl = build_cl_list<S>(ch, o, c, r, 0);
+            lsa = build_sa_list(ch, n, c, r, 0);
+            rare = true;
+        }
         DSTAMP(5);
         } else {
         DSTAMP(4);
@@ -1111,30 +1195,29 @@ __global__ void __launch_bounds__(768) mh_delta_kernel(LaunchArgs a) {
         }
         bool acc;
         if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
-        else
-            acc = !fast_rej &&
-                  u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
+        else if (bd != BOUND_OPEN) acc = bd == BOUND_ACCEPT;
+        else acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
+        // A rejected proposal is undone; after the exact pass of the current configuration
+        // (rare) the state is the current one, and an accepted proposal is re-applied.
+        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer);
         if (acc) {
-            cur_total = sc[0];
             ++accepted;
             o.cmx = o.pmx;
             o.carg = o.parg;
             wild_cnt = wild_star;
+            if (FASTD && bd == BOUND_ACCEPT) {
+                cur_exact = false;
+                cur_iv = star_iv;
+            } else {
+                cur_total = sc[0];
+                if constexpr (FASTD) {
+                    cur_exact = true;
+                    cur_iv = CostIv{cur_total, cur_total};
+                }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = uniform_f(sc[k]);
-            if (writer) commit_swap_zrr(ch, n);
-            wave_sync();
-        } else {
-            const int nb = ch.aux->nb;
-            for (int q = nb - 1; q >= 0; --q) {
-                const DBackup b = ch.aux->b[q];
-                write_pose<S>(ch, o, r, writer, b.k, b.x, b.y, b.ry);
-                if (writer) ch.CPH[b.k] = b.w;
+                for (int k = 0; k < 8; ++k) cur[k] = uniform_f(sc[k]);
             }
-            for (int w = r; w < ch.SW; w += L) ch.SAM[w] = ch.SAMB[w];
-            wave_sync();
-            clearance_delta<S>(ch, o, n, c, ka, kb, r);
-            rels_delta(ch, nr, ka, kb, r);
+            if (writer) commit_swap_zrr(ch, n);
             wave_sync();
         }
         DSTAMP(6);
@@ -1197,6 +1280,7 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_delta_cycles(unsi
 
 // Object slots per lane of the instance that serves n objects.
 static int delta_slots(int n) { return n <= 64 ? 1 : n <= 128 ? 2 : n <= 256 ? 4 : 8; }
+int delta_max_waves(int n) { return delta_max_waves_s(delta_slots(n)); }
 
 size_t delta_lds_bytes(const DeltaLds& lay, int waves_per_wg) {
     return (size_t)lay.hdr + (size_t)waves_per_wg * lay.stride;

@@ -50,6 +50,7 @@ hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg,
 size_t delta_lds_bytes(const DeltaLds& lay, int waves_per_wg);
 hipError_t launch_delta(const LaunchArgs& a, int waves_per_wg, hipStream_t s);
 int delta_blocks_per_cu(int n, int waves_per_wg, size_t lds_bytes);
+int delta_max_waves(int n);  // chains per workgroup the incremental kernel admits
 int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds_bytes);
 hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
                           int64_t chain_offset, mh_summary* out, hipStream_t s);
