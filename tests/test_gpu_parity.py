@@ -637,12 +637,13 @@ def test_stacked_objects_symmetry_ties(mh, orc, hiplib, monkeypatch, step, n, ch
     ("main", 32, 64, 600),
     ("wrap", 24, 64, 500),
     ("syn", 9, 64, 500),
+    ("syn", 256, 16, 1200),  # config 5's room: the incremental kernel's 4-slot instance
 ])
 def test_bound_decision_paths(mh, orc, hiplib, monkeypatch, step, slack, kind, n, chains, steps):
-    """The step bound decides Accept without the exact costs where it can: a certain reject
-    (both step kernels) or, in the full-evaluation kernel, a certain accept that leaves the
-    current total known only as an interval; otherwise the exact costs are computed, the current
-    configuration's too when they are pending. $MH_BOUND_SLACK widens the bound's error
+    """The step bound decides Accept without the exact costs where it can: a certain reject or
+    a certain accept that leaves the current total known only as an interval (both step kernels;
+    the full-evaluation kernel with one object per lane); otherwise the exact costs are computed,
+    the current configuration's too when they are pending. $MH_BOUND_SLACK widens the bound's error
     allowance (still a valid bound), which moves steps from the certain decisions to the exact
     paths: every mix must give the oracle's chains."""
     monkeypatch.setenv("MH_BOUND_SLACK", slack)
