@@ -1140,7 +1140,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     // from the cuRAND XORWOW stream instead of Philox. Plain OP_STEP carries no tracking code.
     constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_T || OP == OP_STEP_XW);
     constexpr bool TRACK = (OP == OP_STEP_T || OP == OP_STEP_XW);
-    using Rng = typename RngOf<OP == OP_STEP_XW, L>::type;
+    // (one chain per wave draws from the wave-batched Philox window, its Box-Muller pairs in LDS)
+    using Rng = typename std::conditional<OP != OP_STEP_XW && L == 64, WaveRngLds,
+                                          typename RngOf<OP == OP_STEP_XW, L>::type>::type;
     constexpr int G = 64 / L;
     const int n = a.rm.n;
     const int lane = threadIdx.x & 63;
@@ -1263,6 +1265,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         bool cur_exact = true;  // (plain steps: false after a proposal accepted on the bound)
         CostIv cur_iv{cur_total, cur_total};
         Rng rng;
+        if constexpr (std::is_same<Rng, WaveRngLds>::value)
+            rng.bsl = reinterpret_cast<float*>(base + F.RNG);
         rng_load(rng, a, chain, m0);
         uint64_t accepted = m0.accepted;
         float best_total = m0.best_total;

@@ -275,6 +275,59 @@ struct WaveRng {
     }
 };
 
+// WaveRng with the window's Box-Muller pairs in LDS (float[2][64] per chain, `bsl`) instead of
+// two registers per lane: the full-evaluation step kernel is held to 96 VGPRs, and the pairs it
+// kept in registers were spilled to scratch at every window fill.
+struct WaveRngLds {
+    uint64_t seed, subseq;
+    uint64_t base;   // first draw of the window
+    uint64_t draws;  // next draw
+    unsigned int w;  // lane i: word base + i
+    float* bsl;      // [i], [64 + i]: box_muller(word base + i, word base + i + 1)
+    int bm_has;
+    float bm_val;
+
+    __device__ __forceinline__ void fill(uint64_t at) {
+        base = at;
+        const WaveWindow ww = wave_window(seed, subseq, at);
+        w = ww.w;
+        const int lane = __lane_id();
+        bsl[lane] = ww.bs;
+        bsl[64 + lane] = ww.bc;
+    }
+    __device__ __forceinline__ void prepare() {
+        if (draws - base > 64 - 16) fill(draws);
+    }
+    __device__ __forceinline__ unsigned int word_at(uint64_t d) const {
+        if (d - base < 64) return (unsigned int)__builtin_amdgcn_readlane((int)w, (int)(d - base));
+        return philox_word(seed, subseq, d);
+    }
+    __device__ __forceinline__ unsigned int next() { return word_at(draws++); }
+    __device__ __forceinline__ float uniform() {
+        return rocrand_device::detail::uniform_distribution(next());
+    }
+    __device__ __forceinline__ float normal() {
+        if (bm_has) {
+            bm_has = 0;
+            return bm_val;
+        }
+        float zs, zc;
+        if (draws - base < 63) {
+            const int i = (int)(draws - base);
+            zs = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[i])));
+            zc = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[64 + i])));
+        } else {
+            const float2 z = box_muller_inl(word_at(draws), word_at(draws + 1));
+            zs = z.x;
+            zc = z.y;
+        }
+        draws += 2;
+        bm_val = zc;
+        bm_has = 1;
+        return zs;
+    }
+};
+
 template <bool XW, int L = 0> struct RngOf { using type = ChainRng; };
 template <> struct RngOf<false, 64> { using type = WaveRng; };
 template <int L> struct RngOf<true, L> { using type = ChainRngXw; };
@@ -313,6 +366,18 @@ __device__ __forceinline__ void rng_load(WaveRng& r, const LaunchArgs& a, int64_
     r.fill(m.draws);
 }
 __device__ __forceinline__ void rng_save(const WaveRng&, const LaunchArgs&, int64_t) {}
+__device__ __forceinline__ void rng_prepare(WaveRngLds& r) { r.prepare(); }
+// (bsl must be set before the load: the first window is filled here)
+__device__ __forceinline__ void rng_load(WaveRngLds& r, const LaunchArgs& a, int64_t chain,
+                                         const ChainMeta& m) {
+    r.seed = a.seed;
+    r.subseq = (uint64_t)(a.chain_offset + chain);
+    r.draws = m.draws;
+    r.bm_has = m.bm_has;
+    r.bm_val = m.bm_val;
+    r.fill(m.draws);
+}
+__device__ __forceinline__ void rng_save(const WaveRngLds&, const LaunchArgs&, int64_t) {}
 __device__ __forceinline__ void rng_save(const ChainRng&, const LaunchArgs&, int64_t) {}
 __device__ __forceinline__ void rng_save(const ChainRngXw& r, const LaunchArgs& a, int64_t chain) {
     unsigned int* w = a.xw + chain * 6;

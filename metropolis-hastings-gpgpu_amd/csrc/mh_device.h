@@ -272,7 +272,7 @@ inline MH_HD constexpr int bank_place_c(int o, unsigned& used) {
 // clearance shapes; the relationship table follows at a run-time offset.
 struct FixedLds {
     int h_room, h_obj, h_frz, h_zero, h_clr;            // workgroup header (h_zero: 4 zero doubles)
-    int P, AUX, PX, PY, CPHF, RMXF, LCL, end;  // per chain
+    int P, AUX, PX, PY, CPHF, RMXF, LCL, RNG, end;  // per chain (RNG: L = 64 only)
 };
 
 inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
@@ -295,6 +295,8 @@ inline MH_HD constexpr FixedLds fixed_lds(int L, int NPL) {
     f.CPHF = bank_place_c(o, dslots); o = f.CPHF + 8 * NC;
     f.RMXF = bank_place_c(o, dslots); o = f.RMXF + 8 * NC;
     f.LCL = bank_place_c(o, dslots);  o = f.LCL + 16 * L;
+    // the Box-Muller pairs of the chain's 64-word Philox window (WaveRngLds, one chain per wave)
+    f.RNG = o; o += L == 64 ? 512 : 0;
     f.end = o;
     return f;
 }
