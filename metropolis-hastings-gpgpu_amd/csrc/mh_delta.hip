@@ -35,8 +35,8 @@
 #if MH_STAMPS
 __device__ unsigned long long g_delta_cycles[8];
 // sums of the Clearance / SurfaceArea list sizes, list overflows, steps that evaluated the
-// rejection bound, steps it rejected
-__device__ unsigned long long g_delta_counts[6];
+// rejection bound, steps it rejected, steps it accepted, exact passes of the current configuration
+__device__ unsigned long long g_delta_counts[8];
 #define DSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t) :: "memory"); cyc[k] += _t - t_last; t_last = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define DSTAMP(k) do { } while (0)
@@ -1128,6 +1128,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         if (r == 0) {
             atomicAdd(&g_delta_counts[4], 1ull);
             atomicAdd(&g_delta_counts[5], (unsigned long long)(bd == BOUND_REJECT ? 1 : 0));
+            atomicAdd(&g_delta_counts[6], (unsigned long long)(bd == BOUND_ACCEPT ? 1 : 0));
         }
 #endif
         float sc[8];
@@ -1181,6 +1182,9 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             lcl = build_cl_list<S>(ch, o, c, r, 0);
             lsa = build_sa_list(ch, n, c, r, 0);
             rare = true;
+#if MH_STAMPS > 1
+            if (r == 0) atomicAdd(&g_delta_counts[7], 1ull);
+#endif
         }
         DSTAMP(5);
         } else {
@@ -1273,7 +1277,7 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_delta_cycles(unsi
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_delta_cycles), sizeof(unsigned long long) * 8) !=
         hipSuccess)
         return -1;
-    return hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_delta_counts), sizeof(unsigned long long) * 6) ==
+    return hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_delta_counts), sizeof(unsigned long long) * 8) ==
                    hipSuccess ? 0 : -1;
 }
 #endif

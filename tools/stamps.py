@@ -30,7 +30,7 @@ def main():
         s.finalize()
         acc_rate = s.summary().accepted / float(chains * iters)
         lanes, cpw, s_kind = s.step_kernel()
-    out = (C.c_ulonglong * 14)()
+    out = (C.c_ulonglong * 16)()
     delta = hasattr(lib, "mh_debug_delta_cycles") and s_kind == "incremental"
     if delta:  # incremental step kernel: per-wavefront stamps, 64/lanes chains per wavefront
         assert lib.mh_debug_delta_cycles(out) == 0
@@ -52,9 +52,11 @@ def main():
               f"{out[11] / steps:.4f}")
     if delta and out[12]:  # counts (MH_STAMPS=2 builds): per step that reached the replay
         steps = chains * iters
-        rep = max(1, out[12] - out[13])
+        rep = max(1, out[12] - out[13] - out[14])
         print(f"  rejection bound evaluated on {out[12] / steps:.4f} of steps, certain reject on "
-              f"{out[13] / steps:.4f}; per replayed step: mean Clearance list "
+              f"{out[13] / steps:.4f}, certain accept on {out[14] / steps:.4f}; exact costs of the "
+              f"current configuration recomputed on {out[15] / steps:.4f}; per replayed step: "
+              f"mean Clearance list "
               f"{out[8] / rep:.2f}, SurfaceArea list {out[9] / rep:.2f}, overflow fractions "
               f"{out[10] / rep:.4f} / {out[11] / rep:.4f}")
 
