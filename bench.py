@@ -106,6 +106,26 @@ def cpu_baseline(room, orc, seed: int, budget_s: float):
                       f" process's affinity, 16 of them the box's per-GPU share)"}
 
 
+def e2e_wrapper(mh, room, chains: int, iters: int, seed: int):
+    """The drop-in entry point end to end (SURVEY.md 8(d) "Also report end-to-end KernelWrapper
+    time"): one KernelWrapperSeeded call on host buffers, as the reference's caller makes it
+    (Kernel.cu:873-984: room upload, chain setup, `iters` MH steps, the final pass and the copy
+    of every chain's points and costs back into the host result), wall-clock timed."""
+    import ctypes as C
+    lib = mh.load_library()
+    g = mh.abi.gpuConfig(chains, 0, 64, 0, 0, iters)
+    t0 = time.perf_counter()
+    res = lib.KernelWrapperSeeded(*room.args(), C.byref(g), C.c_uint64(seed))
+    wall = time.perf_counter() - t0
+    if not res:
+        raise mh.MHError(mh.last_error(lib))
+    lib.KernelFreeResult(res)
+    return {"entry": "KernelWrapperSeeded", "chains": chains, "iterations": iters,
+            "wall_s": wall, "chain_steps_per_s": chains * iters / wall,
+            "result_bytes": chains * (room.n * 24 + 40),
+            "note": "host buffers in, host result out (PCIe both ways); never `value`"}
+
+
 def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str):
     """The committed rocprofv3 PMC record of the step kernel (profiles/pmc_step_kernel_n<N>.json,
     written by tools/pmc_summary.py --json) if it was taken on this workload, else {}."""
@@ -137,6 +157,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-iters", type=int, default=4000,
+                    help="MH steps of the end-to-end KernelWrapperSeeded leg (0: skip)")
     args = ap.parse_args()
     args.iters = max(1, args.iters)
     launches_per_step = -(-args.iters // STEPS_PER_LAUNCH)
@@ -228,6 +250,9 @@ def main() -> int:
 
     out = None
     if rank == 0:
+        e2e = None
+        if world == 1 and args.e2e_iters > 0:
+            e2e = e2e_wrapper(mh, room, args.chains, args.e2e_iters, args.seed)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             orc = graft.load_oracle()
@@ -284,9 +309,13 @@ def main() -> int:
                 # VALU issue utilisation of the profiled launch (tools/pmc_summary.py): busy
                 # SIMD cycles priced per instruction class / (1024 SIMDs x kernel cycles)
                 "valu_issue_util": pmc.get("valu_issue_util"),
-                "pmc_source": pmc.get("source"),
+                # the tracked record this block reads, and the counter summary it was made from
+                "pmc_source": (f"profiles/pmc_step_kernel_n{n}.json" if pmc else None),
+                "pmc_profile": pmc.get("profile"),
             },
             "cpu_baseline": cpu,
+            "e2e_chain_steps_per_s": e2e["chain_steps_per_s"] if e2e else None,
+            "e2e": e2e,
         }
         print(json.dumps(out), flush=True)
     sess.close()

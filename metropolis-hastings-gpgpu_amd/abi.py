@@ -137,6 +137,24 @@ class MHError(RuntimeError):
 _lib = None
 
 
+def _check_build_matches_sources(p: Path) -> None:
+    """The product library must have been built from the sources beside it: build() records
+    their hash (libmhgpu.so.srchash); a library built from other sources is refused."""
+    stamp = p.with_name(p.name + ".srchash")
+    entry = p.parents[1] / "__graft_entry__.py"
+    if not entry.exists():  # an installed copy without the tree: nothing to compare against
+        return
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mh_graft_entry", entry)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    want = mod.source_hash()
+    got = stamp.read_text().strip() if stamp.exists() else "(no record)"
+    if got != want:
+        raise MHError(f"{p} was not built from the sources in this tree (recorded {got[:12]}, "
+                      f"tree {want[:12]}): run __graft_entry__.build()")
+
+
 def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     """Loads libmhgpu.so (built by __graft_entry__.build()). Raises if it is missing."""
     global _lib
@@ -145,6 +163,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     p = Path(path) if path else Path(os.environ.get("MH_LIB", LIB_PATH))
     if not p.exists():
         raise MHError(f"{p} not found: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    if p.resolve() == LIB_PATH.resolve():
+        _check_build_matches_sources(p)
     lib = C.CDLL(str(p))
     room_args = [P(relationshipStruct), P(relationshipAngleStruct), P(positionAndRotation),
                  P(rectangle), P(rectangle), P(vertex), P(vertex), P(Surface)]

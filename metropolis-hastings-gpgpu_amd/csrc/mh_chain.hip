@@ -47,6 +47,30 @@ __device__ unsigned long long g_phase_cycles[16];
 #define MH_PHASE(ch, k, t0) do { } while (0)
 #endif
 
+#ifndef MH_CHECK
+#define MH_CHECK 0  // debug builds: every computed global / LDS index is validated and the first
+                    // violation recorded (mh_debug_check) instead of accessed; product = 0
+#endif
+#if MH_CHECK
+#ifdef MH_CHAIN_STEP_TU
+static __device__ unsigned int g_check[8];
+#else
+__device__ unsigned int g_check[8];  // [0] violations, [1] site, [2] [3] values, [4] chain
+#endif
+__device__ __noinline__ bool mh_check_fail(unsigned site, unsigned v0, unsigned v1) {
+    if (atomicAdd(&g_check[0], 1u) == 0u) {
+        g_check[1] = site;
+        g_check[2] = v0;
+        g_check[3] = v1;
+        g_check[4] = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    }
+    return false;
+}
+#define MH_CK(ok, site, v0, v1) ((ok) ? true : mh_check_fail((site), (unsigned)(v0), (unsigned)(v1)))
+#else
+#define MH_CK(ok, site, v0, v1) (true)
+#endif
+
 namespace mh {
 
 struct Backup {  // the cost-relevant pose of one object (z, rotX, rotZ never enter a cost)
@@ -248,8 +272,22 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
 // uniform `u_acc`, the function returns with *fast set to BOUND_REJECT or BOUND_ACCEPT, the
 // proposal's interval in *star_iv and `out` unset (the symmetry rows and Clearance pairs are
 // set: they come before the bound); otherwise it goes on to the exact costs.
+// eval_costs and propose are always inlined into the step kernels: an out-of-line call that
+// takes references to the kernel's private (stack) objects faulted on MI355X with this toolchain
+// (DESIGN.md "The counting-build fault"; round 2's MH_STAMPS build, where the inliner left
+// eval_costs out of line). tests/test_abi.py checks that no kernel calls either.
+// MH_EVAL_INLINE=-1 builds the out-of-line variant for that experiment.
+#ifndef MH_EVAL_INLINE
+#define MH_EVAL_INLINE 1
+#endif
+#if MH_EVAL_INLINE > 0
+#define MH_EVAL_ATTR __attribute__((always_inline))
+#else
+#define MH_EVAL_ATTR __attribute__((noinline))
+#endif
+
 template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false>
-__device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPose<NPL>& op,
+__device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPose<NPL>& op,
                            int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
@@ -426,7 +464,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
         any_amb |= amb[m];
         float e = 0.0f;
         const double ry1 = pose_ry_var<L, NPL>(op, j1[m], gbase);  // (every lane active)
-        if (row && j1[m] >= 0) {
+        if (row && j1[m] >= 0 && MH_CK(j1[m] < n, 7, j1[m], i)) {
             const ObjP q = ch.P[j1[m]];
             e = sym_val_exact(q.xf, q.yf, ry1, rxs[m], rys[m], (double)rrs[m]);
         }
@@ -519,6 +557,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
             for (int m = NPL - 2; m >= 0; --m) ms = pend[m] ? m : ms;
             const unsigned pm = sel<NPL>(pend, ms);
             const int col = (pm & 1u) ? ka : kb;
+            MH_CK(col >= 0 && col < n, 8, col, pm);
             const ObjP q = ch.P[col];
             const float e = sym_val_exact(q.xf, q.yf, (pm & 1u) ? rya : ryb, sel<NPL>(rxs, ms),
                                           sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
@@ -626,6 +665,7 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
         const double ryj = pose_ry_var<L, NPL>(op, j, gbase);  // (every lane active)
         if (leadp) {
             leadp &= leadp - 1u;
+            MH_CK(j >= 0 && j < n, 9, j, ms);
             const ObjP q = ch.P[j];
             const float e = sym_val_exact(q.xf, q.yf, ryj, sel<NPL>(rxs, ms),
                                           sel<NPL>(rys, ms), (double)sel<NPL>(rrs, ms));
@@ -745,7 +785,8 @@ __device__ void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPo
                     const int i = __builtin_ctzll(bits);
                     bits &= bits - 1;
                     const int pos = ch.PRE[i] + __builtin_popcountll(NZn[i] & below);
-                    ch.LCL[pos] = (double)-overlap(ch.CLA[i], boxj);
+                    if (MH_CK(i < c && pos >= 0 && pos < 2 * L, 6, i, pos))
+                        ch.LCL[pos] = (double)-overlap(ch.CLA[i], boxj);
                 }
                 cnt_cl = cl_total;
                 cl_done = true;
@@ -971,7 +1012,7 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, OwnPose<NPL>& op,
         op.y[m] = here ? y : op.y[m];
         op.ry[m] = here ? ry : op.ry[m];
     }
-    if (writer) {
+    if (writer && MH_CK(k >= 0 && k < ch.rm->n, 4, k, 0)) {
         ObjP p;
         p.xf = (float)x;
         p.yf = (float)y;
@@ -985,7 +1026,7 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, OwnPose<NPL>& op,
 // overwritten objects in ch.aux so a rejection can undo them. Returns the objects it changed
 // (-1: none).
 template <int L, int NPL, class Rng>
-__device__ int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen,
+__device__ MH_EVAL_ATTR int2 propose(Rng& rng, const DevRoom& rm, const unsigned char* frozen,
                         const ChainPtrs& ch, OwnPose<NPL>& op, int r, int gbase, bool writer) {
     const int n = rm.n;
     const int mode = rand_int(rng, 2, 0);
@@ -1089,6 +1130,7 @@ __device__ __forceinline__ void save_best_pose(const ChainPtrs& ch, const OwnPos
 __device__ __forceinline__ void commit_swap_zrr(const ChainPtrs& ch, int n) {
     const int ka = ch.aux->swap_a, kb = ch.aux->swap_b;
     if (ka < 0) return;
+    if (!MH_CK(ka < n && kb >= 0 && kb < n, 1, ka, kb)) return;
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
         double* row = ch.zrr + f * n;
@@ -1103,8 +1145,10 @@ template <int L, int NPL>
 __device__ __forceinline__ void restore(const ChainPtrs& ch, OwnPose<NPL>& op, int r,
                                         bool writer) {
     const int nb = ch.aux->nb;
+    if (!MH_CK(nb >= 0 && nb <= 2, 2, nb, 0)) return;
     for (int q = nb - 1; q >= 0; --q) {
         const Backup b = ch.aux->b[q];
+        if (!MH_CK(b.k >= 0 && b.k < ch.rm->n, 3, b.k, q)) continue;
         write_obj<L, NPL>(ch, op, r, writer, b.k, b.x, b.y, b.ry);
     }
 }
@@ -1177,6 +1221,10 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 
     const int64_t chain = ((int64_t)blockIdx.x * waves_per_wg + wave) * G + g;
     if (chain >= a.n_chains) return;
+    // (debug builds: the host's layout agrees with the compile-time one and fits the launch)
+    MH_CK(a.lay.AUX == F.AUX && a.lay.PX == F.PX && a.lay.LCL == F.LCL && a.lay.stride >= F.end &&
+              a.lay.hdr >= F.h_clr,
+          13, a.lay.AUX, F.AUX);
 
     unsigned char* base = lds + a.lay.hdr + (wave * G + g) * a.lay.stride;
     ChainPtrs ch;
@@ -1285,6 +1333,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             MH_STAMP(ts);
             rng_prepare(rng);
             const int2 kk = propose<L, NPL>(rng, *rm_l, frozen, ch, op, r, gbase, writer);
+            MH_CK(kk.x < n && kk.y < n && kk.x >= -1 && kk.y >= -1, 11, kk.x, kk.y);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
@@ -1314,6 +1363,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     // poses in the backup slots so that restore() re-applies them.
                     const int nb = ch.aux->nb;
                     const int k0 = nb > 0 ? ch.aux->b[0].k : 0, k1 = nb > 1 ? ch.aux->b[1].k : 0;
+                    MH_CK(nb >= 0 && nb <= 2 && k0 >= 0 && k0 < n && k1 >= 0 && k1 < n, 10,
+                          k0 | (nb << 16), k1);
                     const Backup s0 = read_obj<L, NPL>(op, k0, gbase);
                     const Backup s1 = read_obj<L, NPL>(op, k1, gbase);
                     restore<L, NPL>(ch, op, r, writer);
@@ -1411,7 +1462,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
             m.best_total = best_total;
             m.rung = m0.rung;
-            a.meta[chain] = m;
+            if (MH_CK(chain >= 0 && chain < a.n_chains, 12, (unsigned)chain, 0)) a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
         ClPairs clf;
@@ -1767,6 +1818,13 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
     hipLaunchKernelGGL(mh_summary_kernel, dim3(1), dim3(1024), 0, s, costs, meta, n, chain_offset, out);
     return hipGetLastError();
 }
+
+#if MH_CHECK
+extern "C" __attribute__((visibility("default"))) int mh_debug_check(unsigned int* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check), sizeof(unsigned int) * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsigned long long* out) {

@@ -415,7 +415,7 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
 // PairWise / PairWiseAngle terms of the relationships touching ka or kb (or all, ka = -2).
 // The hit test reads the relationship objects from LDS; the records themselves (ranges,
 // normalisers) come from HBM, for the few relationships a move touches.
-__device__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
+__device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
     uint64_t pend = 0;
     int t = 0;
     for (int q = r; q < nr; q += L, ++t) {
@@ -488,7 +488,7 @@ __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& 
 
 // Non-zero SurfaceArea terms in the reference's order, negated: positions [lo, lo + cap_sa) go
 // to LSA[pos - lo]. Returns the total count. With `sum`, this lane's partial sum of its terms.
-__device__ int build_sa_list(const DeltaPtrs& ch, int n, int c, int r, int lo,
+__device__ __forceinline__ int build_sa_list(const DeltaPtrs& ch, int n, int c, int r, int lo,
                              float* sum = nullptr) {
     int base = 0;
     float acc = 0.0f;

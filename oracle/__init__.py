@@ -80,6 +80,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_pick_object.restype = C.c_int
     lib.orc_index_n_draws.argtypes = [C.c_int]
     lib.orc_index_n_draws.restype = C.c_longlong
+    lib.orc_set_step_offlimits.argtypes = [C.c_int]
+    lib.orc_set_step_offlimits.restype = None
     lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.orc_accept.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.orc_accept.restype = C.c_int
@@ -171,6 +173,13 @@ def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int =
             d[:, :, k] = raw[:, :, 8 * k:8 * k + 8].copy().view(np.float64)[:, :, 0]
         return d, c8, a
     return np.frombuffer(bytes(buf), dtype=np.float32).reshape(chains, n, 6).copy(), c8, a
+
+
+def set_step_offlimits(on: bool) -> None:
+    """OffLimits in every step's Costs() (True, the reference's loop Kernel.cu:785-828) or only
+    for the output configurations (False: the same outputs bit for bit, faster; OffLimits never
+    enters totalCosts, :547). Process-wide."""
+    load().orc_set_step_offlimits(1 if on else 0)
 
 
 def index_n_draws(reset: bool = False) -> int:

@@ -501,7 +501,24 @@ float orc_off_limits(const orc_room* room, const positionAndRotation* cfg) {
 
 /* Kernel.cu:516-550. PairWise is the PRODUCT of the distance and angle terms (:518); the
  * total leaves OffLimits out (:547) and is summed in float in the reference's order. */
+/* OffLimitsCosts in every step's Costs() (1, the reference's loop, :516-550 via :800) or only
+ * for the configurations a chain outputs (0). OffLimits never enters totalCosts (:547), so no
+ * accept decision depends on it, and a chain's output costs are Costs() of its output
+ * configuration either way: 0 gives the same outputs bit for bit in about half the time at
+ * N = 64 (the parity tests use it; the CPU baseline keeps the reference's loop). */
+static int g_step_offlimits = 1;
+
+void orc_set_step_offlimits(int on) { g_step_offlimits = on != 0; }
+
+static void costs_ex(const orc_room* room, const positionAndRotation* cfg, resultCosts* out,
+                     int with_ol);
+
 void orc_costs(const orc_room* room, const positionAndRotation* cfg, resultCosts* out) {
+    costs_ex(room, cfg, out, 1);
+}
+
+static void costs_ex(const orc_room* room, const positionAndRotation* cfg, resultCosts* out,
+                     int with_ol) {
     const Surface* s = room->srf;
     float pw = (float)(orc_pairwise(room, cfg) * orc_pairwise_angle(room, cfg));
     out->PairWiseCosts = s->WeightPairWise * pw;
@@ -511,7 +528,7 @@ void orc_costs(const orc_room* room, const positionAndRotation* cfg, resultCosts
     out->FocalPointCosts = s->WeightFocalPoint * fp;
     float sym = orc_symmetry(room, cfg);
     out->SymmetryCosts = s->WeightSymmetry * sym;
-    float ol = orc_off_limits(room, cfg);
+    float ol = with_ol ? orc_off_limits(room, cfg) : 0.0f;
     out->OffLimitsCosts = s->WeightOffLimits * ol;
     float cl = orc_clearance(room, cfg);
     out->ClearanceCosts = s->WeightClearance * cl;
@@ -712,7 +729,7 @@ static void chain_init(const chain_job* job, int64_t local, chain_state* st) {
     else
         orc_rng_init(&st->r, job->seed, gid);
     memcpy(st->cur, job->cfg, sizeof(positionAndRotation) * n);
-    orc_costs(job->room, st->cur, &st->cc);
+    costs_ex(job->room, st->cur, &st->cc, g_step_offlimits);
     /* Best-of-chain, the reference's commented-out intent: cfgBest := cfgCurrent
      * (Kernel.cu:779-782); star replaces best when it improves, before Accept (:808-816). */
     st->bc = st->cc;
@@ -728,7 +745,7 @@ static void chain_steps(const chain_job* job, chain_state* st, int steps, double
     for (int it = 0; it < steps; ++it) {
         memcpy(st->star, st->cur, sizeof(positionAndRotation) * n);
         orc_propose(job->room, st->star, &st->r);
-        orc_costs(job->room, st->star, &sc);
+        costs_ex(job->room, st->star, &sc, g_step_offlimits);
         if (job->track && (job->track == MH_TRACK_LOWEST ? sc.totalCosts < st->bc.totalCosts
                                                          : sc.totalCosts > st->bc.totalCosts)) {
             memcpy(st->best, st->star, sizeof(positionAndRotation) * n);
@@ -749,7 +766,9 @@ static void chain_output(const chain_job* job, const chain_state* st, int64_t sl
     const int n = job->room->srf->nObjs;
     /* with tracking the output is cfgBest / bestCosts (Kernel.cu:840-860, commented out) */
     const positionAndRotation* out = job->track ? st->best : st->cur;
-    const resultCosts oc = job->track ? st->bc : st->cc;
+    resultCosts oc = job->track ? st->bc : st->cc;
+    if (!g_step_offlimits)  /* the output configuration's own OffLimits (see g_step_offlimits) */
+        oc.OffLimitsCosts = job->room->srf->WeightOffLimits * orc_off_limits(job->room, out);
     if (job->out_points) {
         point* p = job->out_points + slot * n;
         for (int i = 0; i < n; ++i) {

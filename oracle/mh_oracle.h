@@ -90,6 +90,9 @@ int orc_rand_int(orc_rng* r, int max, int min);
 int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r);
 /* How many times pick_object drew index nObjs (u == 1.0f) in this process; reset if asked. */
 long long orc_index_n_draws(int reset);
+/* OffLimits in every step's Costs() (1, default: the reference's loop) or only for the output
+ * configurations (0: identical outputs, faster). Process-wide. */
+void orc_set_step_offlimits(int on);
 
 /* One proposal (Kernel.cu:576-704) applied in place to cfg (nObjs entries). */
 void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r);

@@ -3,6 +3,7 @@ as C and C++, and the host-side validation paths of KernelWrapper (which return 
 call). Compute entry points are exercised by tests/test_gpu_parity.py on the MI355X."""
 import ctypes as C
 import re
+import struct
 import subprocess
 from pathlib import Path
 
@@ -37,6 +38,52 @@ def test_library_is_gfx950_code(mh, tmp_path):
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
                          capture_output=True, text=True, cwd=tmp_path)
     assert "gfx950" in (out.stdout + out.stderr) or b"gfx950" in lib.read_bytes()
+
+
+def _device_functions(lib_path, tmp_path):
+    """Names of the FUNC symbols of every gfx950 code object in the library's offload bundles
+    (one bundle per HIP translation unit, concatenated in .hip_fatbin)."""
+    fatbin = tmp_path / "fatbin.bin"
+    subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objcopy", f"--dump-section=.hip_fatbin={fatbin}",
+                    str(lib_path), str(tmp_path / "stripped.so")], check=True)
+    data = fatbin.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    names, objects = set(), 0
+    at = data.find(magic)
+    while at >= 0:
+        count = struct.unpack_from("<Q", data, at + 24)[0]
+        p = at + 32
+        for _ in range(count):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" not in triple:
+                continue
+            co = tmp_path / f"co{objects}.o"
+            co.write_bytes(data[at + off:at + off + size])
+            objects += 1
+            out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-s", "--wide", str(co)],
+                                 check=True, capture_output=True, text=True).stdout
+            for ln in out.splitlines():
+                f = ln.split()
+                if len(f) >= 8 and f[3] == "FUNC":
+                    names.add(f[7])
+        at = data.find(magic, at + 1)
+    return names, objects
+
+
+def test_step_kernels_make_no_calls(mh, tmp_path):
+    """Every device function that takes references to a kernel's private objects (eval_costs,
+    propose, the incremental kernel's helpers) is inlined: an out-of-line call of eval_costs
+    faulted on MI355X (DESIGN.md "The counting-build fault"). Only the value-only Box-Muller
+    helpers may stay out of line."""
+    names, objects = _device_functions(mh.LIB_PATH, tmp_path)
+    assert objects == 4  # mh_chain, mh_chain_xw, mh_chain_best, mh_delta
+    kernels = {n for n in names if "_kernel" in n}
+    assert any("mh_kernelILi64ELi1ELi1E" in n for n in kernels)
+    helpers = names - kernels
+    allowed = {"_ZN2mhL10box_mullerEjj", "_ZN2mhL17curand_box_mullerEjj"}
+    assert helpers <= allowed, sorted(helpers - allowed)
 
 
 @pytest.mark.parametrize("lang,compiler", [("c", "gcc"), ("c++", "g++")])

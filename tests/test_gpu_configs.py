@@ -4,21 +4,27 @@ the reference edges that short runs do not reach -- each chain bit for bit again
 
 * config 1: the console harness's 32-object room through KernelWrapper, 10,000 chains x 100 steps;
 * config 2: the 8-object room, all 1,024 chains x 10k steps;
-* config 3: 64 chains sampled by global id out of a 65,536-chain, 100k-step session;
+* config 3: 256 chains sampled by global id out of a 65,536-chain, 100k-step session (the
+  bench's own session: same room, seed and length), plus the device summary of all 65,536
+  chains (the bench's mean_final_cost) against the downloaded costs;
 * config 4: one rank's shard (global ids 7*65,536 ...), the 2-rank bench.py launcher path, and
   KernelWrapper's in-process $MH_DEVICES sharding (unmeasured on 8 GPUs: the driver runs those);
-* config 5: 8 chains sampled out of a 32,768-chain, 10k-step session of the 256-object room;
+* config 5: 64 chains sampled out of a 32,768-chain, 10k-step session of the 256-object room;
 * the index-n pick (u == 1.0f, Kernel.cu:566-574,598-602) on every RNG path, from a searched
   fixture (tests/golden/find_index_n.py);
 * KernelWrapper's $MH_SEED against KernelWrapperSeeded (Kernel.cu:873,943);
 * the incremental kernel's list-overflow windows (a room where every Clearance pair overlaps).
 
 Every check asserts zero forked chains and reports the count as a ParityReport warning, which
-`pytest -q` keeps in its summary.
+`pytest -q` keeps in its summary. The long oracle runs leave OffLimits out of the per-step
+Costs() (oracle.set_step_offlimits(False)): it never enters totalCosts (Kernel.cu:547), so the
+chains and their output costs are the same bit for bit, in about half the time.
 """
+import contextlib
 import json
 import os
 import socket
+import warnings
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -27,13 +33,28 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from parity_util import check_chains
+from parity_util import ParityReport, check_chains
 
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
 GOLDEN = json.loads((ROOT / "tests" / "golden" / "golden.json").read_text())
 HOST_THREADS = 16  # the GPU box's CPU share per GPU
+
+
+@contextlib.contextmanager
+def _fast_oracle(orc):
+    orc.set_step_offlimits(False)
+    try:
+        yield
+    finally:
+        orc.set_step_offlimits(True)
+
+
+def _spread(total, blocks, per):
+    """`blocks` block starts of `per` chains spread evenly over [0, total), the last block
+    ending at the last chain."""
+    return [round(k * (total - per) / (blocks - 1)) for k in range(blocks)]
 
 
 def _oracle_blocks(orc, room, starts, per, steps, seed, threads_each):
@@ -50,7 +71,7 @@ def _oracle_blocks(orc, room, starts, per, steps, seed, threads_each):
 def _session_sampled(mh, orc, room, chains, steps, seed, starts, per, threads_each, offset=0):
     """Runs a full-size session (launches queued asynchronously) while the oracle runs the
     sampled blocks, then returns both."""
-    with mh.Session(room, chains, seed=seed, chain_offset=offset) as s:
+    with mh.Session(room, chains, seed=seed, chain_offset=offset) as s, _fast_oracle(orc):
         s.run(steps)
         ref_pts, ref_costs, ids = _oracle_blocks(orc, room, [offset + b for b in starts], per,
                                                  steps, seed, threads_each)
@@ -89,31 +110,53 @@ def test_config2_full_length(mh, orc, hiplib):
     check_chains("config 2 (N=8, 1024 x 10k)", pts, costs, ref_pts, ref_costs, report=True)
 
 
+def _check_summary(name, summ, costs, offset=0):
+    """The device summary (mh_summary_kernel: what bench.py all-gathers and reports as
+    mean_final_cost / best_final_cost / best_chain) against the downloaded final costs of every
+    chain: the same count, the same best total at the lowest such id, and the mean of all chains'
+    totals (a double sum in another order: equal to ~1e-15)."""
+    tot = costs[:, 0].astype(np.float64)
+    assert summ.n_chains == len(costs)
+    assert summ.best_total == costs[:, 0].max()
+    assert summ.best_chain == offset + int(np.argmax(costs[:, 0]))
+    mean = summ.sum_total / summ.n_chains
+    assert mean == pytest.approx(tot.mean(), rel=1e-12, abs=0)
+    warnings.warn(f"{name}: device summary of all {len(costs)} chains: mean final total "
+                  f"{mean:.9g} (host mean of the downloaded costs {tot.mean():.9g}), best "
+                  f"{summ.best_total:.9g} at chain {summ.best_chain}", ParityReport)
+
+
 def test_config3_full_length_sampled(mh, orc, hiplib):
-    """Config 3: a 65,536-chain session run for the config's 100,000 steps; 64 chains sampled
-    across the id range (8 blocks of 8) against the oracle by global id."""
+    """Config 3: a 65,536-chain session run for the config's 100,000 steps -- bench.py's own
+    workload (room, seed 42, 25 x 4,000 steps) -- with 256 chains sampled across the id range
+    (16 blocks of 16) against the oracle by global id, and the device summary of all chains
+    (bench.py's mean_final_cost) against the downloaded costs."""
     room = mh.synthetic_room(64)
     chains, steps, seed = 65536, 100_000, 42
-    starts = [0, 9360, 18720, 28080, 37440, 46800, 56160, 65528]
+    starts = _spread(chains, 16, 16)
     pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
-        mh, orc, room, chains, steps, seed, starts, 8, 2)
-    check_chains("config 3 (N=64, 65536 x 100k, 64 sampled)", sp, sc, rp, rc, ids=ids,
+        mh, orc, room, chains, steps, seed, starts, 16, 1)
+    assert len(ids) == 256 and len(set(ids.tolist())) == 256
+    check_chains("config 3 (N=64, 65536 x 100k, 256 sampled)", sp, sc, rp, rc, ids=ids,
                  report=True)
-    assert summ.n_chains == chains and summ.best_total == costs[:, 0].max()
+    _check_summary("config 3", summ, costs)
     assert _in_room(room, pts)
 
 
 def test_config5_full_length_sampled(mh, orc, hiplib):
     """Config 5: the 256-object room, a 32,768-chain session for 10,000 steps (incremental
-    kernel, 5 chains per CU); 8 chains sampled by global id against the oracle."""
+    kernel); 64 chains sampled by global id (16 blocks of 4 across the id range) against the
+    oracle, and the device summary of all chains against the downloaded costs."""
     room = mh.synthetic_room(256)
     chains, steps, seed = 32768, 10_000, 42
-    starts = [0, 4681, 9362, 14043, 18724, 23405, 28086, 32767]
+    starts = _spread(chains, 16, 4)
     pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
-        mh, orc, room, chains, steps, seed, starts, 1, 1)
-    check_chains("config 5 (N=256, 32768 x 10k, 8 sampled)", sp, sc, rp, rc, ids=ids,
+        mh, orc, room, chains, steps, seed, starts, 4, 1)
+    assert len(ids) == 64 and len(set(ids.tolist())) == 64
+    check_chains("config 5 (N=256, 32768 x 10k, 64 sampled)", sp, sc, rp, rc, ids=ids,
                  report=True)
-    assert summ.n_chains == chains and _in_room(room, pts)
+    _check_summary("config 5", summ, costs)
+    assert _in_room(room, pts)
 
 
 def test_config4_rank7_shard(mh, orc, hiplib):
@@ -126,9 +169,7 @@ def test_config4_rank7_shard(mh, orc, hiplib):
         mh, orc, room, chains, steps, seed, starts, 8, 2, offset=offset)
     check_chains("config 4 rank-7 shard (N=64, 65536 x 5k, 64 sampled)", sp, sc, rp, rc,
                  ids=ids, report=True)
-    assert summ.n_chains == chains
-    assert offset <= summ.best_chain < offset + chains
-    assert summ.best_total == costs[summ.best_chain - offset, 0]
+    _check_summary("config 4 rank-7 shard", summ, costs, offset=offset)
 
 
 def _free_port():

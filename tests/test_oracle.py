@@ -413,3 +413,22 @@ def test_tempering_at_one_temperature_permutes_plain_chains(mh, orc):
         a = sorted(costs[g * K:(g + 1) * K].view(np.uint32).tolist())
         b = sorted(pcosts[g * K:(g + 1) * K].view(np.uint32).tolist())
         assert a == b
+
+
+@pytest.mark.parametrize("kw", [{}, {"track": 2}, {"temps": 4, "swap_interval": 7},
+                                {"rng": 1}], ids=["plain", "track", "tempering", "xorwow"])
+def test_step_offlimits_knob_keeps_outputs(mh, orc, kw):
+    """set_step_offlimits(False) leaves OffLimits out of the per-step Costs() (it never enters
+    totalCosts, Kernel.cu:547) and evaluates it for the output configurations only: every
+    output -- poses, all eight costs, accept counts -- is the same bit for bit."""
+    room = mh.synthetic_room(24)
+    a = orc.run_chains(room, 8, 150, 31, threads=4, **kw)
+    orc.set_step_offlimits(False)
+    try:
+        b = orc.run_chains(room, 8, 150, 31, threads=4, **kw)
+    finally:
+        orc.set_step_offlimits(True)
+    for x, y in zip(a, b):
+        x, y = np.asarray(x), np.asarray(y)
+        assert x.dtype == y.dtype and np.array_equal(x.view(np.uint8), y.view(np.uint8))
+    assert np.any(a[1][:, 6] != 0)  # the room's objects do overlap: OffLimits is exercised

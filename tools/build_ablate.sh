@@ -2,6 +2,8 @@
 # Timing-only variants of libmhgpu.so with phases compiled out (MH_ABLATE bitmask):
 #   1 symmetry rows, 2 per-object atan2/cos, 4 ordered sums, 8 SurfaceArea/Clearance pairs,
 #   16 PairWise/Angle, 32 Box-Muller. Results are WRONG by construction; only time matters.
+# `check` validates every computed index in the full-evaluation kernel and records the first
+# violation (mh_debug_check) instead of accessing it; `countscheck` is the counting build with it.
 # `stamps` builds the per-phase cycle-stamp diagnostic (tools/stamps.py) instead; `dblK`
 # runs phase bit K twice with identical results (cost probe: the trajectory is unchanged).
 set -e
@@ -12,6 +14,10 @@ for M in "$@"; do
   case "$M" in
     stamps) DEF=-DMH_STAMPS=1 ;;
     counts) DEF=-DMH_STAMPS=2 ;;
+    countscheck) DEF="-DMH_STAMPS=2 -DMH_CHECK=1" ;;
+    check) DEF=-DMH_CHECK=1 ;;
+    countsinl) DEF="-DMH_STAMPS=2 -DMH_EVAL_INLINE=1" ;;
+    noinl) DEF=-DMH_EVAL_INLINE=-1 ;;
     wpe*) DEF=-DMH_WAVES_PER_EU=${M#wpe} ;;
     dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
     *) DEF=-DMH_ABLATE=$M ;;

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--chains", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=1000, help="MH steps per launch")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--profile", default=None,
+                    help="the tracked profiles/ copy of this summary (recorded in the JSON)")
     a = ap.parse_args()
     c, meta = load(a.tag_dir, a.kernel)
     if not c:
@@ -87,7 +89,7 @@ def main():
                "valu_issue_util": d.get("valu_issue_util"),
                "valu_issue_util_flat": d.get("valu_issue_util_flat"),
                "valu_pricing": "2 cyc/VALU; +2 fp64 add/mul/fma, cvt, f32 trans; +6 f64 trans",
-               "source": os.path.normpath(a.tag_dir)}
+               "source": os.path.normpath(a.tag_dir), "profile": a.profile}
         with open(a.json, "w") as fh:
             json.dump(rec, fh, indent=1)
         print("wrote", a.json)

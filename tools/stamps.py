@@ -26,10 +26,19 @@ def main():
     mh = graft.load_package()
     lib = mh.load_library()
     with mh.Session(mh.synthetic_room(n), chains, seed=42) as s:
-        s.run(iters)
-        s.finalize()
-        acc_rate = s.summary().accepted / float(chains * iters)
         lanes, cpw, s_kind = s.step_kernel()
+        print(f"[stamps] session created: {lanes} lanes/chain, {cpw} chains/workgroup, {s_kind}",
+              flush=True)
+        s.run(iters)
+        print("[stamps] run launched", flush=True)
+        s.finalize()
+        print("[stamps] finalize launched", flush=True)
+        acc_rate = s.summary().accepted / float(chains * iters)
+    if hasattr(lib, "mh_debug_check"):  # MH_CHECK builds: the first index violation, if any
+        ck = (C.c_uint * 8)()
+        assert lib.mh_debug_check(ck) == 0
+        print(f"[check] violations={ck[0]} first site={ck[1]} values=({ck[2]}, {ck[3]}) "
+              f"wave={ck[4]}", flush=True)
     out = (C.c_ulonglong * 16)()
     delta = hasattr(lib, "mh_debug_delta_cycles") and s_kind == "incremental"
     if delta:  # incremental step kernel: per-wavefront stamps, 64/lanes chains per wavefront
