@@ -238,7 +238,14 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     g.dlay = mh::make_delta_layout(n, c, r);
     const char* e = getenv("MH_DELTA");
     g.delta = e && *e ? atoi(e) != 0 : n > 128;
-    const int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
+    int want_w = getenv("MH_DELTA_WAVES") ? atoi(getenv("MH_DELTA_WAVES")) : 0;
+    if (want_w != 0 && (want_w < 1 || want_w > mh::delta_max_waves(n))) {
+        // (a tuning knob: clamped to the kernel's launch bound, never a silent kernel change)
+        const int w = want_w < 1 ? 1 : mh::delta_max_waves(n);
+        fprintf(stderr, "mhgpu: MH_DELTA_WAVES=%d is outside 1..%d for %d objects; using %d\n",
+                want_w, mh::delta_max_waves(n), n, w);
+        want_w = w;
+    }
     int best_chains = -1;
     g.dL = 64;
     g.dwaves = 0;
@@ -440,9 +447,10 @@ bool upload(T** dst, const std::vector<T>& src, hipStream_t st) {
 
 // Orders work about to be queued on `st` after everything the session queued before, on
 // whichever stream that was (its own stream for the setup, a caller's stream for a run; the
-// event was recorded there, so that stream may since have been destroyed).
+// event was recorded there, so that stream may since have been destroyed -- and a new stream
+// can reuse a destroyed one's handle, so the wait is made even when the handles are equal).
 bool order_after_last(mh_session* s, hipStream_t st) {
-    if (st != s->last) MH_TRY_HIP(hipStreamWaitEvent(st, s->done, 0));
+    MH_TRY_HIP(hipStreamWaitEvent(st, s->done, 0));
     return true;
 }
 
@@ -523,14 +531,33 @@ bool session_finalize(mh_session* s, hipStream_t st) {
     return record_done(s, st);
 }
 
+// Copies `bytes` from device memory into a caller's (pageable) host buffer on the session's
+// stream, ordered after the session's work: the host range is page-locked for the copy so the
+// DMA runs straight into it and does not serialise against other devices' work (KernelWrapper
+// runs one host thread per device); where it cannot be locked, a plain staged copy.
+bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes) {
+    if (bytes == 0) return true;
+    hipStream_t st = s->stream;
+    if (!order_after_last(s, st)) return false;
+    // ($MH_DOWNLOAD_PAGEABLE=1: the staged copy only, for the A/B of the two)
+    static const bool pageable = getenv("MH_DOWNLOAD_PAGEABLE") && atoi(getenv("MH_DOWNLOAD_PAGEABLE"));
+    const bool locked = !pageable && hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
+    if (!locked) (void)hipGetLastError();  // (clear the sticky error of the failed lock)
+    MH_TRY_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+    const hipError_t e = hipStreamSynchronize(st);
+    if (locked) (void)hipHostUnregister(host);
+    MH_TRY_HIP(e);
+    return record_done(s, st);
+}
+
+// The session's final points and costs, after all of its queued work (an event wait, so another
+// session's work on the same device is not waited for).
 bool session_download(mh_session* s, point* pts, resultCosts* costs) {
     MH_TRY_HIP(hipSetDevice(s->device));
-    MH_TRY_HIP(hipDeviceSynchronize());
     const size_t n = (size_t)s->room.rm.n;
-    if (pts && s->n_chains > 0)
-        MH_TRY_HIP(hipMemcpy(pts, s->d_pts, sizeof(point) * n * s->n_chains, hipMemcpyDeviceToHost));
-    if (costs && s->n_chains > 0)
-        MH_TRY_HIP(hipMemcpy(costs, s->d_costs, sizeof(resultCosts) * s->n_chains, hipMemcpyDeviceToHost));
+    if (s->n_chains <= 0) return true;
+    if (pts && !copy_out(s, pts, s->d_pts, sizeof(point) * n * s->n_chains)) return false;
+    if (costs && !copy_out(s, costs, s->d_costs, sizeof(resultCosts) * s->n_chains)) return false;
     return true;
 }
 
