@@ -148,7 +148,7 @@ def _check_build_matches_sources(p: Path) -> None:
     spec = importlib.util.spec_from_file_location("_mh_graft_entry", entry)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    want = mod.source_hash()
+    want = mod.source_hash(("-DMH_CHECK=1",) if p.name == "libmhgpu_check.so" else ())
     got = stamp.read_text().strip() if stamp.exists() else "(no record)"
     if got != want:
         raise MHError(f"{p} was not built from the sources in this tree (recorded {got[:12]}, "
@@ -163,7 +163,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     p = Path(path) if path else Path(os.environ.get("MH_LIB", LIB_PATH))
     if not p.exists():
         raise MHError(f"{p} not found: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
-    if p.resolve() == LIB_PATH.resolve():
+    if p.resolve() in (LIB_PATH.resolve(), LIB_PATH.with_name("libmhgpu_check.so").resolve()):
         _check_build_matches_sources(p)
     lib = C.CDLL(str(p))
     room_args = [P(relationshipStruct), P(relationshipAngleStruct), P(positionAndRotation),

@@ -47,30 +47,6 @@ __device__ unsigned long long g_phase_cycles[16];
 #define MH_PHASE(ch, k, t0) do { } while (0)
 #endif
 
-#ifndef MH_CHECK
-#define MH_CHECK 0  // debug builds: every computed global / LDS index is validated and the first
-                    // violation recorded (mh_debug_check) instead of accessed; product = 0
-#endif
-#if MH_CHECK
-#ifdef MH_CHAIN_STEP_TU
-static __device__ unsigned int g_check[8];
-#else
-__device__ unsigned int g_check[8];  // [0] violations, [1] site, [2] [3] values, [4] chain
-#endif
-__device__ __noinline__ bool mh_check_fail(unsigned site, unsigned v0, unsigned v1) {
-    if (atomicAdd(&g_check[0], 1u) == 0u) {
-        g_check[1] = site;
-        g_check[2] = v0;
-        g_check[3] = v1;
-        g_check[4] = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    }
-    return false;
-}
-#define MH_CK(ok, site, v0, v1) ((ok) ? true : mh_check_fail((site), (unsigned)(v0), (unsigned)(v1)))
-#else
-#define MH_CK(ok, site, v0, v1) (true)
-#endif
-
 namespace mh {
 
 struct Backup {  // the cost-relevant pose of one object (z, rotX, rotZ never enter a cost)
@@ -708,8 +684,11 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             bt.fp = -cph[0];
             bt.afp = fabsf(bt.fp);
             bt.sym = -sym.mx[0];
+            bt.symw = r < n ? (float)(n - r) * sym.mx[0] : 0.0f;  // (row r: position r)
             bt.cl = -clsum;
             bt.kcl = kcl;
+            bt.clpos = 0.0f;  // (no position credit: the list positions are not formed here)
+            bt.pwd = bt.angd = 0.0;
             bt.sa = -((sac[0].x + sac[0].y + sac[0].z + sac[0].w) +
                       (sao[0].x + sao[0].y + sao[0].z + sao[0].w));
             bt.pw = -(float)rpw[0];
@@ -1312,6 +1291,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         float cur_total = m0.costs[0];
         bool cur_exact = true;  // (plain steps: false after a proposal accepted on the bound)
         CostIv cur_iv{cur_total, cur_total};
+#if MH_CHECK
+        float chk_cur = cur_total;  // (check builds: the current total, always exact)
+#endif
         Rng rng;
         if constexpr (std::is_same<Rng, WaveRngLds>::value)
             rng.bsl = reinterpret_cast<float*>(base + F.RNG);
@@ -1352,6 +1334,36 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             eval_costs<L, NPL, false, true, FASTK>(a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y,
                                                     cls, cl, u_acc, cur_iv, &fast, &star_iv);
             MH_STAMP(ts);
+#if MH_CHECK
+            // Check builds verify every decision the bound takes against the exact costs: the
+            // proposal's exact total lies in the bound's interval, the current total in the
+            // carried one, and a certain REJECT / ACCEPT is Accept's decision.
+            float chk_star = sc[0];
+            if constexpr (FASTK) {
+                if (fast != BOUND_OPEN) {
+                    float cx[8];
+                    SymRows<NPL> sx;
+                    ClPairs clx;
+                    eval_costs<L, NPL, false, true>(a, ch, op, r, gbase, cx, sx, sym, kk.x, kk.y,
+                                                    clx, cl);
+                    chk_star = uniform_f(cx[0]);
+                    if (r == 0) atomicAdd(&g_check[5], 1u);
+                    const bool acc_x =
+                        u_acc < accept_threshold(kBeta * ((double)chk_star - (double)chk_cur));
+                    if (r == 0) {
+                        MH_CK(chk_star >= star_iv.lo && chk_star <= star_iv.hi, 22,
+                              __float_as_uint(chk_star), __float_as_uint(star_iv.hi - star_iv.lo));
+                        MH_CK(fast != BOUND_REJECT || !acc_x, 20, __float_as_uint(chk_star),
+                              __float_as_uint(chk_cur));
+                        MH_CK(fast != BOUND_ACCEPT || acc_x, 21, __float_as_uint(chk_star),
+                              __float_as_uint(chk_cur));
+                    }
+                }
+                if (r == 0)
+                    MH_CK(chk_cur >= cur_iv.lo && chk_cur <= cur_iv.hi, 23,
+                          __float_as_uint(chk_cur), __float_as_uint(cur_iv.hi - cur_iv.lo));
+            }
+#endif
             if constexpr (FASTK) {
                 // (rare: ~2% of config-3 steps; the hint lets the allocator keep the step's
                 // values in registers around this path: 80 -> 72 bytes of scratch per lane,
@@ -1385,6 +1397,11 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     cur_total = uniform_f(cx[0]);
                     cur_exact = true;
                     cur_iv = CostIv{cur_total, cur_total};
+#if MH_CHECK
+                    if (r == 0)
+                        MH_CK(cur_total == chk_cur, 24, __float_as_uint(cur_total),
+                              __float_as_uint(chk_cur));
+#endif
                     wave_sync();
                     if (u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total))) {
                         restore<L, NPL>(ch, op, r, writer);  // the proposal again
@@ -1416,6 +1433,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 sym = ss;
                 cl = cls;
                 ++accepted;
+#if MH_CHECK
+                if constexpr (FASTK) chk_cur = chk_star;
+#endif
                 if (exact) {
                     cur_total = sc[0];
                     if constexpr (FASTK) {

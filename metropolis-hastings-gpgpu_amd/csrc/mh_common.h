@@ -16,6 +16,28 @@
 #define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
 #endif
 
+#ifndef MH_CHECK
+#define MH_CHECK 0  // debug builds: computed global / LDS indices validated and every decision of
+                    // the rejection bound verified against the exact costs, the first violation
+                    // recorded (mh_debug_check / mh_debug_check_delta); product = 0
+#endif
+#if MH_CHECK
+static __device__ unsigned int g_check[8];  // (per translation unit) [0] violations, [1] site,
+                                            // [2] [3] values, [4] wave, [5] checks made
+__device__ __forceinline__ bool mh_check_fail(unsigned site, unsigned v0, unsigned v1) {
+    if (atomicAdd(&g_check[0], 1u) == 0u) {
+        g_check[1] = site;
+        g_check[2] = v0;
+        g_check[3] = v1;
+        g_check[4] = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    }
+    return false;
+}
+#define MH_CK(ok, site, v0, v1) ((ok) ? true : mh_check_fail((site), (unsigned)(v0), (unsigned)(v1)))
+#else
+#define MH_CK(ok, site, v0, v1) (true)
+#endif
+
 namespace mh {
 
 struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
@@ -708,13 +730,44 @@ struct BoundTerms {
     float nx, ny, anx, any;  // VisualBalance area * x, area * y (Kernel.cu:200-201)
     float fp, afp;           // FocalPoint -cos(phi) (:277)
     float sym;               // Symmetry -(row max) (:314), all <= 0
+    float symw;              // sum of (n - i) |term i| over this lane's rows i (the sequential
+                             // float sum's rounding weights, below); n |sym| is always valid
     float cl;                // Clearance -overlap (:429), all <= 0
     int kcl;                 // Clearance terms pre-summed by this lane
+    float clpos;             // sum of pos |term| over this lane's Clearance terms at their
+                             // positions pos in the non-zero list (0: no position credit)
     float sa;                // SurfaceArea -overlap (:463-479), all <= 0
     float pw, ang, aang;     // PairWise -(range term) (<= 0), PairWiseAngle (:222, :249-253)
+    double pwd, angd;        // the same PairWise / PairWiseAngle partial sums in double
+                             // (bound_decide<true>: the two sums in fp64)
     int k;                   // most terms any lane pre-sums into any other partial sum (the
                              // same value on every lane: it enters the uniform bound)
 };
+
+// One butterfly level of a double: v + (its partner's v), both halves moved by bfly<OFF>.
+template <int OFF>
+__device__ __forceinline__ double bfly_add(double v) {
+    const int2 w = *reinterpret_cast<int2*>(&v);
+    int2 o;
+    o.x = bfly<OFF>(w.x);
+    o.y = bfly<OFF>(w.y);
+    return v + *reinterpret_cast<double*>(&o);
+}
+
+// Sum of a double over the 64 lanes of the wavefront, uniform: six butterfly levels, six fp64
+// additions per lane in a fixed order (error <= 6 * 2^-53 * sum |v| beyond the lanes' own).
+__device__ __forceinline__ double wave_dsum(double v) {
+    v = bfly_add<1>(v);
+    v = bfly_add<2>(v);
+    v = bfly_add<4>(v);
+    v = bfly_add<8>(v);
+    v = bfly_add<16>(v);
+    v = bfly_add<32>(v);
+    int2 w = *reinterpret_cast<int2*>(&v);
+    w.x = __builtin_amdgcn_readfirstlane(w.x);
+    w.y = __builtin_amdgcn_readfirstlane(w.y);
+    return *reinterpret_cast<double*>(&w);
+}
 
 // Sum of v over the 64 lanes of the wavefront, uniform (an SGPR): in-row butterflies (DPP
 // quad_perm, row_half_mirror, row_mirror), then row_bcast15 / row_bcast31 carry the row sums
@@ -783,10 +836,19 @@ enum { BOUND_OPEN = 0, BOUND_REJECT = 1, BOUND_ACCEPT = 2 };
 // Whether Accept's decision for this proposal is already certain, for a chain that owns the
 // wavefront: BOUND_REJECT / BOUND_ACCEPT, or BOUND_OPEN (the exact costs are needed). n objects,
 // c clearances, nrel relationships, ncl non-zero Clearance terms; `cur` holds the current
-// total. The arithmetic after the lane sums is fp32 on wave-uniform values; every intermediate
-// has at most ~30 roundings on quantities no larger than M (below), so 64 U M covers them, and
-// the proposal's exact total lies in t +- 1.25 e. `star` receives an interval around it that
-// also absorbs the rounding of its own ends (e >= 64 U |t|, so 0.25 e does).
+// total. The arithmetic after the lane sums is fp32 on wave-uniform values (with DPW the
+// PairWise and PairWiseAngle sums and their product are fp64: their fp32 error dominated the
+// bound at N = 256, where PairWise is most of the total); the proposal's exact total lies in
+// t +- 1.25 e. `star` receives an interval around it that also absorbs the rounding of its own
+// ends (e >= 8 U |t|, so 0.25 e does).
+//
+// e is the sum of term-by-term error bounds: each sum's (the reference's sequential rounding
+// and this estimate's), each composition step of Costs() (the e1, e2 and 12 U terms), and the
+// roundings no term covers -- the reference's five float additions of the total (:547), each
+// at most U times a partial sum of the components, whose magnitudes add up to at most cabs
+// below; the two additions forming t; and the decision's own arithmetic on t, e and cur (t +
+// 1.25 e, minus cur, the star ends): 8 U cabs + 3 U (|t| + |cur|) covers them.
+template <bool DPW = false>
 __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
                                             const BoundTerms& bt, float u, CostIv cur,
                                             CostIv& star, float slack = 1.0f) {
@@ -796,25 +858,30 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
                 lsa = rm.w_sa * bt.sa;
     const float lin = (lfp + lsym) + (lcl + lsa);
     const float afp = fabsf(rm.w_fp) * bt.afp;
-    // A sequential sum of m terms in a float accumulator is within (m - 1) U (1 + m U) sum |t|
-    // of the exact sum (one rounding to nearest per add); in a double accumulator within
-    // m 2^-53 (1 + m 2^-53) sum |t|. Our estimate: terms rounded to float once, k pre-summed per
-    // lane, a six-level tree: (k + 7) U sum |t|. "26" covers both second-order parts for
-    // m < 2^20. FocalPoint accumulates in double, Symmetry, Clearance and SurfaceArea in float.
-    const float eacc = 0x1p-29f * (float)(n + nrel);  // (double accumulators, in units of U)
-    const float elin = (26.0f + kf + eacc) * U * afp + (n + 26.0f + kf) * U * fabsf(lsym) +
-                       (ncl + 26.0f + (float)bt.kcl) * U * fabsf(lcl) +
-                       (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) +
-                       12.0f * U * (afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa));
-    // sums of |t| for VisualBalance: one sum of |area x| + |area y| bounds both coordinates'
-    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin, bt.anx + bt.any, bt.aang};
+    const float alin = afp + fabsf(lsym) + fabsf(lcl) + fabsf(lsa);  // (lanes' |components|)
+    // A sequential sum of m terms in a float accumulator (Symmetry :314, Clearance :429) is
+    // within U sum_q |partial sum q| (1 + m U) of the exact sum: one rounding to nearest per
+    // add, and zero terms do not round. With terms of one sign the partial sums add up to
+    // sum_q (m - q) |t_q|, t_q the term at position q: per lane, symw, and ncl |cl| - clpos for
+    // the compacted Clearance terms (clpos = 0 gives the plain m U sum |t|). In a double
+    // accumulator (FocalPoint, PairWise, PairWiseAngle) the same is m 2^-53 sum |t| (eacc, in
+    // units of U). This estimate: terms rounded to float once, k pre-summed per lane, a
+    // six-level tree: (k + 7) U sum |t|. "26" covers the second-order parts for m < 2^20.
+    const float eacc = 0x1p-29f * (float)(n + nrel);
+    const float wsym = fabsf(rm.w_sym) * bt.symw;
+    const float wcl = fabsf(rm.w_cl) * fmaxf(0.0f, (float)ncl * fabsf(bt.cl) - bt.clpos);
+    const float elin = (26.0f + kf + eacc) * U * afp + (26.0f + kf) * U * fabsf(lsym) +
+                       U * wsym + (26.0f + (float)bt.kcl) * U * fabsf(lcl) + U * wcl +
+                       (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) + 12.0f * U * alin;
+    // sum[6] bounds sum |area x| and sum |area y| for VisualBalance, and the components' sum
+    // of magnitudes (alin) for the catch-all term
+    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin, bt.anx + bt.any + alin,
+                           bt.aang};
     float sum[8];
     wave_fsum8(part, sum);
-    const float s_nx = sum[0], s_ny = sum[1], s_pw = sum[2], s_ang = sum[3], s_lin = sum[4],
-                s_elin = sum[5];
-    // (each partial of anx + any is rounded once more: 1.25 e below absorbs it)
+    const float s_nx = sum[0], s_ny = sum[1], s_lin = sum[4], s_elin = sum[5];
     const float a_nx = fmaxf(fabsf(s_nx), sum[6]), a_ny = fmaxf(fabsf(s_ny), sum[6]),
-                a_ang = fmaxf(fabsf(s_ang), sum[7]);
+                a_ang = fmaxf(fabsf(sum[3]), sum[7]);
     // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
     const float id = fabsf(rm.inv_denom);
     const float cv = (n + 26.0f + kf) * U;  // (float accumulators, Kernel.cu:200-201)
@@ -827,29 +894,47 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const float dvb = dfx + dfy + 2.0f * U * (fabsf(vb) + dfx + dfy);
     const float o2 = rm.w_vb * vb;
     const float e2 = fabsf(rm.w_vb) * (dvb + 3.0f * U * (fabsf(vb) + dvb));
-    // PairWise x PairWiseAngle (Kernel.cu:518)
-    const float cr = (26.0f + kf + eacc) * U;  // (double accumulators, :222, :249-253)
-    const float epw = cr * fabsf(s_pw), eang = cr * a_ang;
-    const float pa = s_pw * s_ang;
-    const float dpa = fabsf(s_pw) * eang + fabsf(s_ang) * epw + epw * eang;
+    // PairWise x PairWiseAngle (Kernel.cu:518), both sums accumulated in double (:222, :249-253)
+    float pa, dpa;
+    if constexpr (DPW) {
+        // fp64 lane partial sums and tree: within (k + 8) 2^-53 sum |t| of the exact sums, the
+        // reference's within nrel 2^-53 sum |t|; the product rounded once to double and then,
+        // like the reference's (float)(pw * ang), to float
+        const double spw = wave_dsum(bt.pwd), sang = wave_dsum(bt.angd);
+        const double pad = spw * sang;
+        const float cr = (float)((double)(nrel + bt.k + 12) * 0x1p-53);
+        const float epw = cr * (float)fabs(spw) * (1.0f + 64.0f * U),
+                    eang = cr * a_ang * (1.0f + 64.0f * U);
+        pa = (float)pad;
+        dpa = (float)fabs(spw) * eang + (float)fabs(sang) * epw + epw * eang +
+              (float)(0x1p-52 * fabs(pad));
+    } else {
+        const float s_pw = sum[2], s_ang = sum[3];
+        const float cr = (26.0f + kf + eacc) * U;  // (double accumulators)
+        const float epw = cr * fabsf(s_pw), eang = cr * a_ang;
+        pa = s_pw * s_ang;
+        dpa = fabsf(s_pw) * eang + fabsf(s_ang) * epw + epw * eang;
+    }
     const float o1 = rm.w_pw * pa;
     const float e1 = fabsf(rm.w_pw) * (dpa + 3.0f * U * (fabsf(pa) + dpa));
-    // total (Kernel.cu:547) and its upper end
+    // total (Kernel.cu:547) and its ends
     const float t = (o1 + o2) + s_lin;
     const float acur = fmaxf(fabsf(cur.lo), fabsf(cur.hi));
-    const float m = fabsf(o1) + fabsf(o2) + fabsf(s_lin) + e1 + e2 + s_elin + acur +
-                    fabsf(vb) + fabsf(fx) + fabsf(fy) + fabsf(rm.w_pw) * fabsf(pa);
+    const float cabs = fabsf(o1) + e1 + fabsf(o2) + e2 + sum[6];
     const float e = slack * (e1 + e2 + s_elin + 12.0f * U * (fabsf(o1) + e1 + fabsf(o2) + e2) +
-                             64.0f * U * m);
+                             8.0f * U * cabs + 3.0f * U * (fabsf(t) + acur));
     const float x = (float)kBeta * ((t + 1.25f * e) - cur.lo);   // beta (star - cur), upper end
     const float xl = (float)kBeta * ((t - 1.25f * e) - cur.hi);  // and lower end
     // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
     const float lu = __logf(u);
     // Reject: x <= lu - 1e-4 (the compares are NaN-false: an invalid bound is never certain).
-    // Accept: accept_threshold is 1 for beta (star - cur) >= 0, so u < 1 decides; otherwise
-    // exp(beta (star - cur)) (> exp(-24)) exceeds u when log(u) < xl - 1e-4.
+    // Accept: the threshold min(1, exp(beta (star - cur))) is at most 1, so u == 1.0f (which
+    // the (0, 1] uniform draws, ~2^-25 of draws) is never accepted; otherwise the threshold is 1
+    // for beta (star - cur) >= 0, and exp(beta (star - cur)) (> exp(-24)) exceeds u when
+    // log(u) < xl - 1e-4. (Round 2 accepted u == 1.0f whenever xl > 1e-4: a certain ACCEPT
+    // against Accept's rejection, found by tools/bound_check.py.)
     const bool rej = x <= lu - 1e-4f && x > -1e30f;
-    const bool acc = (xl >= 0.0f && u < 1.0f) || (xl > -23.9f && lu < xl - 1e-4f);
+    const bool acc = u < 1.0f && (xl >= 0.0f || (xl > -23.9f && lu < xl - 1e-4f));
     star.lo = t - 1.5f * e;
     star.hi = t + 1.5f * e;
     // the chain's first lane decides, so the decision is wave-uniform by construction

@@ -446,9 +446,9 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
 template <int S>
 __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& o, int c, int r,
                                              int lo, float* sum = nullptr,
-                                             int* cnt_own = nullptr) {
+                                             int* cnt_own = nullptr, float* possum = nullptr) {
     int base = 0;
-    float acc = 0.0f;
+    float acc = 0.0f, accp = 0.0f;  // (accp: sum of pos |term|, the bound's position weights)
     int own = 0;
     for (int cb = 0; cb < c; cb += L) {
         const int ci = cb + r;
@@ -472,6 +472,7 @@ __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& 
                     word &= word - 1;
                     const float v = -overlap(A, obj_box(ch, j));
                     acc += v;
+                    accp = fmaf((float)pos, -v, accp);
                     if (pos >= lo && pos < lo + ch.cap_cl) ch.LCL[pos - lo] = v;
                     ++pos;
                 }
@@ -482,6 +483,7 @@ __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& 
     if (sum) {
         *sum = acc;
         *cnt_own = own;
+        *possum = accp;
     }
     return base;
 }
@@ -531,7 +533,9 @@ __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, con
                                         int nr, int r) {
     BoundTerms bt;
     bt.nx = bt.ny = bt.anx = bt.any = bt.fp = bt.afp = bt.sym = bt.cl = bt.sa = 0.0f;
+    bt.symw = bt.clpos = 0.0f;
     bt.pw = bt.ang = bt.aang = 0.0f;
+    bt.pwd = bt.angd = 0.0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {
         const int i = t * L + r;
@@ -546,13 +550,14 @@ __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, con
             bt.fp += w;
             bt.afp += fabsf(w);
             bt.sym -= o.pmx[t];
+            bt.symw = fmaf((float)(n - i), o.pmx[t], bt.symw);  // (row i: position i)
         }
     }
-    for (int q = r; q < nr; q += L) {
-        const float tp = (float)ch.RPW[q], ta = (float)ch.RANG[q];
-        bt.pw += tp;
-        bt.ang += ta;
-        bt.aang += fabsf(ta);
+    for (int q = r; q < nr; q += L) {  // (summed in double: bound_decide<true>)
+        const double tp = ch.RPW[q], ta = ch.RANG[q];
+        bt.pwd += tp;
+        bt.angd += ta;
+        bt.aang += fabsf((float)ta);
     }
     bt.k = max(max((n + L - 1) / L, (nr + L - 1) / L), 4 * ((c + n + L - 1) / L));  // uniform
     return bt;
@@ -1067,6 +1072,9 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
 #endif
+#if MH_CHECK
+    float chk_cur = cur_total;  // (check builds: the current total, always exact)
+#endif
 
 #pragma clang loop unroll(disable)
     for (int it = 0; it < a.iterations; ++it) {
@@ -1108,21 +1116,22 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         int bd = BOUND_OPEN;
         CostIv star_iv{0.0f, 0.0f};
         float u_acc = 0.0f;
-        float clsum = 0.0f, sasum = 0.0f;
+        float clsum = 0.0f, sasum = 0.0f, clpos = 0.0f;
         int kcl = 0;
-        const int cnt_cl = build_cl_list<S>(ch, o, c, r, 0, &clsum, &kcl);
+        const int cnt_cl = build_cl_list<S>(ch, o, c, r, 0, &clsum, &kcl, &clpos);
         const int cnt_sa = build_sa_list(ch, n, c, r, 0, &sasum);
         if constexpr (FASTD) {
             u_acc = rng.uniform();
             BoundTerms bt = delta_bound_terms<S>(ch, o, n, c, nr, r);
             bt.cl = clsum;
             bt.kcl = kcl;
+            bt.clpos = clpos;
             bt.sa = sasum;
             // (not on a launch's last step: it ends with the current costs exact, through the
             // exact pass below when they are not)
             if (it + 1 < a.iterations)
-                bd = bound_decide(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_iv, star_iv,
-                                  a.bound_slack);
+                bd = bound_decide<true>(*rm_l, n, c, nr, cnt_cl, bt, u_acc, cur_iv, star_iv,
+                                        a.bound_slack);
         }
 #if MH_STAMPS > 1
         if (r == 0) {
@@ -1130,6 +1139,30 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             atomicAdd(&g_delta_counts[5], (unsigned long long)(bd == BOUND_REJECT ? 1 : 0));
             atomicAdd(&g_delta_counts[6], (unsigned long long)(bd == BOUND_ACCEPT ? 1 : 0));
         }
+#endif
+#if MH_CHECK
+        // Check builds verify every decision the bound takes against the exact costs (the
+        // replay of the lists just built): the proposal's exact total lies in the bound's
+        // interval, the current total in the carried one, a certain REJECT / ACCEPT is Accept's.
+        float chk_star = 0.0f;
+        if (FASTD && bd != BOUND_OPEN) {
+            float ro[8];
+            replay_config<S>(ch, o.pmx, o, n, cnt_cl, cnt_sa, r, ro);
+            chk_star = uniform_f(ro[0]);
+            const bool acc_x = u_acc < accept_threshold(kBeta * ((double)chk_star - (double)chk_cur));
+            if (r == 0) {
+                atomicAdd(&g_check[5], 1u);
+                MH_CK(chk_star >= star_iv.lo && chk_star <= star_iv.hi, 22,
+                      __float_as_uint(chk_star), __float_as_uint(star_iv.hi - star_iv.lo));
+                MH_CK(bd != BOUND_REJECT || !acc_x, 20, __float_as_uint(chk_star),
+                      __float_as_uint(chk_cur));
+                MH_CK(bd != BOUND_ACCEPT || acc_x, 21, __float_as_uint(chk_star),
+                      __float_as_uint(chk_cur));
+            }
+        }
+        if (FASTD && r == 0)
+            MH_CK(chk_cur >= cur_iv.lo && chk_cur <= cur_iv.hi, 23, __float_as_uint(chk_cur),
+                  __float_as_uint(cur_iv.hi - cur_iv.lo));
 #endif
         float sc[8];
         bool rare = false;  // the exact pass of the current configuration ran (below)
@@ -1161,6 +1194,10 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 #pragma unroll
                 for (int k = 0; k < 8; ++k) cur[k] = uniform_f(ro[k]);
                 cur_total = cur[0];
+#if MH_CHECK
+                if (r == 0) MH_CK(cur_total == chk_cur, 24, __float_as_uint(cur_total),
+                                  __float_as_uint(chk_cur));
+#endif
                 cur_exact = true;
                 cur_iv = CostIv{cur_total, cur_total};
                 break;
@@ -1206,6 +1243,9 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer);
         if (acc) {
             ++accepted;
+#if MH_CHECK
+            chk_cur = bd == BOUND_OPEN ? sc[0] : chk_star;
+#endif
             o.cmx = o.pmx;
             o.carg = o.parg;
             wild_cnt = wild_star;
@@ -1270,6 +1310,13 @@ hipError_t launch_delta_s(const LaunchArgs& a, int waves_per_wg, hipStream_t str
 }
 
 }  // namespace
+
+#if MH_CHECK
+extern "C" __attribute__((visibility("default"))) int mh_debug_check_delta(unsigned int* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check), sizeof(unsigned int) * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_delta_cycles(unsigned long long* out) {

@@ -80,6 +80,8 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_pick_object.restype = C.c_int
     lib.orc_index_n_draws.argtypes = [C.c_int]
     lib.orc_index_n_draws.restype = C.c_longlong
+    lib.orc_u1_uphill_draws.argtypes = [C.c_int]
+    lib.orc_u1_uphill_draws.restype = C.c_longlong
     lib.orc_set_step_offlimits.argtypes = [C.c_int]
     lib.orc_set_step_offlimits.restype = None
     lib.orc_propose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -173,6 +175,12 @@ def run_chains(room, chains: int, iterations: int, seed: int, chain_begin: int =
             d[:, :, k] = raw[:, :, 8 * k:8 * k + 8].copy().view(np.float64)[:, :, 0]
         return d, c8, a
     return np.frombuffer(bytes(buf), dtype=np.float32).reshape(chains, n, 6).copy(), c8, a
+
+
+def u1_uphill_draws(reset: bool = False) -> int:
+    """Accept draws of u == 1.0f against an uphill proposal (threshold exactly 1, so Accept
+    rejects, Kernel.cu:706-713) that the oracle's chains have seen."""
+    return int(load().orc_u1_uphill_draws(1 if reset else 0))
 
 
 def set_step_offlimits(on: bool) -> None:

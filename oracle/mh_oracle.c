@@ -627,6 +627,17 @@ void orc_propose(const orc_room* room, positionAndRotation* cfg, orc_rng* r) {
     }
 }
 
+/* Accept draws of u == 1.0f (the (0,1] uniform's top value) against an uphill proposal, whose
+ * threshold min(1, exp(...)) is exactly 1 and so rejects it (test diagnostic: lets a test prove
+ * that a fixture exercises this edge of Kernel.cu:706-713). */
+static long long g_u1_uphill;
+
+long long orc_u1_uphill_draws(int reset) {
+    const long long v = __atomic_load_n(&g_u1_uphill, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_u1_uphill, 0, __ATOMIC_RELAXED);
+    return v;
+}
+
 /* Kernel.cu:706-713: maximises the total; exp in double, rounded to float. */
 int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
     float u = orc_rng_uniform(r);
@@ -637,6 +648,7 @@ int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
 /* Accept at inverse temperature beta (parallel tempering; beta = BETA is Accept itself). */
 int orc_accept_at(double cost_star, double cost_cur, double beta, orc_rng* r) {
     float u = orc_rng_uniform(r);
+    if (u == 1.0f && cost_star > cost_cur) __atomic_add_fetch(&g_u1_uphill, 1, __ATOMIC_RELAXED);
     float a = fminf(1.0f, (float)exp(beta * (cost_star - cost_cur)));
     return u < a;
 }

@@ -90,6 +90,8 @@ int orc_rand_int(orc_rng* r, int max, int min);
 int orc_pick_object(const positionAndRotation* cfg, int n, orc_rng* r);
 /* How many times pick_object drew index nObjs (u == 1.0f) in this process; reset if asked. */
 long long orc_index_n_draws(int reset);
+/* Accept draws of u == 1.0f against an uphill proposal seen in this process (diagnostic). */
+long long orc_u1_uphill_draws(int reset);
 /* OffLimits in every step's Costs() (1, default: the reference's loop) or only for the output
  * configurations (0: identical outputs, faster). Process-wide. */
 void orc_set_step_offlimits(int on);

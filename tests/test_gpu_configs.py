@@ -266,6 +266,29 @@ def test_index_n_pick_redrawn(mh, orc, hiplib, monkeypatch, case, path):
     check_chains(f"index-n chain {cid} ({path[0]})", pts, costs, rp, rc, ids=[cid])
 
 
+@pytest.mark.parametrize("path", STEP_PATHS, ids=[p[0] for p in STEP_PATHS])
+@pytest.mark.parametrize("case", GOLDEN["u1_accept"], ids=lambda c: f"N{c['n']}-chain{c['chain']}")
+def test_accept_draw_one_rejects_uphill(mh, orc, hiplib, monkeypatch, case, path):
+    """A chain whose Accept draws u == 1.0f (the (0, 1] uniform's top value) against an uphill
+    proposal: the threshold min(1, exp(...)) is exactly 1, so Accept rejects (Kernel.cu:706-713).
+    The rejection bound must not certainly accept it (round 2's bound did; found by
+    tools/bound_check.py). Fixture from tests/golden/find_u1_accept.py; bit for bit against the
+    oracle on every step kernel and RNG path."""
+    for k, v in path[1].items():
+        monkeypatch.setenv(k, v)
+    room = mh.synthetic_room(case["n"])
+    cid, steps, seed = case["chain"], case["steps"], case["seed"]
+    orc.u1_uphill_draws(reset=True)
+    rp, rc, _ = orc.run_chains(room, 1, steps, seed, chain_begin=cid)
+    assert orc.u1_uphill_draws() >= 1
+    with mh.Session(room, 1, seed=seed, chain_offset=cid) as s:
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+    check_chains(f"u == 1.0f uphill chain {cid} N={case['n']} ({path[0]})", pts, costs, rp, rc,
+                 ids=[cid])
+
+
 def _crowded_room(mh, n):
     """Every clearance box overlaps every object box at every reachable pose: a 0.5 m room
     (translations clamp to it, Kernel.cu:613-630) and boxes of 0.5-2 m."""

@@ -432,3 +432,18 @@ def test_step_offlimits_knob_keeps_outputs(mh, orc, kw):
         x, y = np.asarray(x), np.asarray(y)
         assert x.dtype == y.dtype and np.array_equal(x.view(np.uint8), y.view(np.uint8))
     assert np.any(a[1][:, 6] != 0)  # the room's objects do overlap: OffLimits is exercised
+
+
+def test_u1_accept_fixture_exercises_the_edge(mh, orc):
+    """The u == 1.0f fixtures (tests/golden/find_u1_accept.py) do draw Accept's u == 1.0f
+    against an uphill proposal in the oracle, at the recorded step and not before."""
+    import json
+    from pathlib import Path
+    g = json.loads((Path(__file__).with_name("golden") / "golden.json").read_text())
+    assert g["u1_accept"]
+    for case in g["u1_accept"]:
+        room = mh.synthetic_room(case["n"])
+        for steps, expect in ((case["step"] - 1, 0), (case["step"], 1)):
+            orc.u1_uphill_draws(reset=True)
+            orc.run_chains(room, 1, steps, case["seed"], chain_begin=case["chain"])
+            assert orc.u1_uphill_draws() == expect, (case, steps)

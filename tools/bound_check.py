@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Verifies every decision the rejection bound takes, on real chains: the MH_CHECK build
+(metropolis-hastings-gpgpu_amd/libmhgpu_check.so, made by __graft_entry__.build()) also computes the exact costs of every
+proposal the bound decided and checks that the exact total lies in the bound's interval, that
+the current total lies in the interval it carries, and that a certain REJECT / ACCEPT is
+Accept's own decision (Kernel.cu:706-713); the first violation is recorded.
+    python tools/bound_check.py [--quick]      (on the GPU box; prints one line per case)"""
+import ctypes as C
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "metropolis-hastings-gpgpu_amd" / "libmhgpu_check.so"  # (__graft_entry__.build())
+SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept rejects",
+         22: "exact total outside the bound's interval",
+         23: "current total outside the carried interval",
+         24: "exact pass of the current configuration differs from the carried total"}
+
+# (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
+# object far outside the proven symmetry range, "negw" flips the weights' signs.
+CASES = [("syn", 64, 8192, 2000, "full"), ("syn", 256, 2048, 1500, "incremental"),
+         ("syn", 8, 1024, 5000, "full"), ("syn", 100, 2048, 1500, "full"),
+         ("syn", 100, 2048, 1500, "incremental"), ("syn", 160, 1024, 1000, "incremental"),
+         ("wrap", 64, 2048, 2000, "full"), ("manyrel", 200, 1024, 1000, "incremental"),
+         ("wrap", 256, 1024, 1000, "incremental"),
+         ("negw", 64, 2048, 2000, "full"), ("negw", 256, 1024, 1000, "incremental"),
+         ("wild", 64, 1024, 1000, "full"), ("wild", 256, 512, 500, "incremental")]
+
+
+def room_of(mh, kind, n):
+    if kind == "manyrel":  # more relationships than objects (R > N + 1)
+        return mh.synthetic_room(n, n_rel=3 * n + 5)
+    room = mh.synthetic_room(n)
+    if kind == "wrap":  # angle ranges crossing zero: the fmodf branch of Kernel.cu:245-250
+        for k in range(room.srf.nRelationships):
+            room.rsa[k].angleMin = 7 * 3.1416 / 4
+            room.rsa[k].angleMax = 3.1416 / 4
+    if kind == "negw":
+        for f in ("WeightPairWise", "WeightVisualBalance", "WeightSymmetry", "WeightClearance"):
+            setattr(room.srf, f, -getattr(room.srf, f))
+    if kind == "wild":
+        for i in range(n):
+            room.cfg[i].x *= 3.0e15
+            room.cfg[i].y *= -2.0e15
+    return room
+
+
+def one(kind, n, chains, steps, kernel):
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as graft
+    mh = graft.load_package()
+    os.environ["MH_DELTA"] = "1" if kernel == "incremental" else "0"
+    lib = mh.load_library(str(LIB))
+    mh.abi._lib = lib  # the Session wrapper uses the module's library
+    room = room_of(mh, kind, n)
+    with mh.Session(room, chains, seed=4242 + n) as s:
+        assert s.step_kernel()[2] == kernel, s.step_kernel()
+        s.run(steps)
+        s.finalize()
+        _, costs = s.download()
+    ck = (C.c_uint * 8)()
+    fn = lib.mh_debug_check_delta if kernel == "incremental" else lib.mh_debug_check
+    assert fn(ck) == 0
+    site = SITES.get(ck[1], str(ck[1]))
+    print(f"[bound] {kind} N={n} {kernel}: {chains} x {steps} steps, {ck[5]} bound decisions "
+          f"checked, violations {ck[0]}" + (f" (first: {site}, values {ck[2]:#x} {ck[3]:#x})"
+                                            if ck[0] else ""), flush=True)
+    return ck[0] == 0
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--one":
+        kind, n, chains, steps, kernel = sys.argv[2], *map(int, sys.argv[3:6]), sys.argv[6]
+        sys.exit(0 if one(kind, n, chains, steps, kernel) else 1)
+    quick = "--quick" in sys.argv
+    ok = True
+    for kind, n, chains, steps, kernel in CASES:
+        if quick:
+            chains, steps = max(64, chains // 8), max(200, steps // 4)
+        rc = subprocess.run([sys.executable, __file__, "--one", kind, str(n), str(chains),
+                             str(steps), kernel], timeout=300).returncode
+        ok &= rc == 0
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
