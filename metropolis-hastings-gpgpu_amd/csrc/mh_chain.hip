@@ -1134,6 +1134,10 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch, OwnPose<NPL>& op, i
 
 // ---- the kernel ---------------------------------------------------------------------------
 
+// Steps of plain chains decide on the rejection bound when a chain owns the wavefront with one
+// object per lane.
+#define FASTK_OF(L, NPL) ((NPL) == 1 && (L) == 64 && !(MH_ABLATE & 4))
+
 // Waves per SIMD the register allocator must leave room for. The plain step kernel with one
 // chain per wavefront and one object per lane (config 3) is held to 5: its LDS then admits five
 // 4-wave workgroups per CU, and 20 resident chains measured 4.47e8 chain-steps/s against 4.20e8
@@ -1326,7 +1330,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             // already rejects skips the exact sums (eval_costs FAST).
             // A proposal the bound accepts is taken without its exact costs: the current total is
             // then known as an interval (cur_iv) until a step needs it exactly (below).
-            constexpr bool FASTK = !TRACK && NPL == 1 && L == 64 && !(MH_ABLATE & 4);
+            constexpr bool FASTK = !TRACK && FASTK_OF(L, NPL);
             int fast = BOUND_OPEN;
             CostIv star_iv{0.0f, 0.0f};
             float u_acc = 0.0f;
@@ -1335,6 +1339,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                                                     cls, cl, u_acc, cur_iv, &fast, &star_iv);
             MH_STAMP(ts);
 #if MH_CHECK
+            if constexpr (FASTK)
+                if (r == 0) mh_count_decision(fast, true);
             // Check builds verify every decision the bound takes against the exact costs: the
             // proposal's exact total lies in the bound's interval, the current total in the
             // carried one, and a certain REJECT / ACCEPT is Accept's decision.
@@ -1368,6 +1374,21 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 // (rare: ~2% of config-3 steps; the hint lets the allocator keep the step's
                 // values in registers around this path: 80 -> 72 bytes of scratch per lane,
                 // 4.81e8 -> 4.84e8 chain-steps/s)
+                // The proposal's exact total often decides against the current total's interval
+                // alone (decide_exact_star); only otherwise is the current configuration made
+                // exact.
+                if (__builtin_expect(fast == BOUND_OPEN && !cur_exact, 0)) {
+                    const int d2 = decide_exact_star(sc[0], cur_iv, u_acc, kBeta);
+#if MH_CHECK
+                    if (r == 0 && d2 != BOUND_OPEN) {
+                        const bool acc_x = u_acc < accept_threshold(
+                                               kBeta * ((double)sc[0] - (double)chk_cur));
+                        MH_CK(acc_x == (d2 == BOUND_ACCEPT), 25, __float_as_uint(sc[0]),
+                              __float_as_uint(chk_cur));
+                    }
+#endif
+                    if (d2 != BOUND_OPEN) fast = d2 + 32;  // (decided; the costs are exact)
+                }
                 if (__builtin_expect(fast == BOUND_OPEN && !cur_exact, 0)) {
                     // The decision needs the current configuration's exact costs: undo the
                     // proposal, evaluate the current configuration incrementally from the
@@ -1398,9 +1419,11 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     cur_exact = true;
                     cur_iv = CostIv{cur_total, cur_total};
 #if MH_CHECK
-                    if (r == 0)
+                    if (r == 0) {
                         MH_CK(cur_total == chk_cur, 24, __float_as_uint(cur_total),
                               __float_as_uint(chk_cur));
+                        atomicAdd(&g_decide[3], 1ull);
+                    }
 #endif
                     wave_sync();
                     if (u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total))) {
@@ -1426,7 +1449,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 if (fast == BOUND_OPEN)
                     acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
                 else
-                    acc = fast == BOUND_ACCEPT || fast == BOUND_ACCEPT + 1;
+                    acc = fast == BOUND_ACCEPT || fast == BOUND_ACCEPT + 1 ||
+                          fast == BOUND_ACCEPT + 32;
                 exact = fast != BOUND_ACCEPT;
             } else acc = accept(rng, sc[0], cur_total);
             if (acc) {
@@ -1471,6 +1495,11 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 12; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
+#endif
+#if MH_CHECK
+        if (!TRACK && FASTK_OF(L, NPL) && r == 0)  // a launch ends with exact current costs
+            MH_CK(ch.aux->cur[0] == chk_cur, 26, __float_as_uint(ch.aux->cur[0]),
+                  __float_as_uint(chk_cur));
 #endif
         if (writer) {
             ChainMeta m;
@@ -1843,6 +1872,11 @@ hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64
 extern "C" __attribute__((visibility("default"))) int mh_debug_check(unsigned int* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check), sizeof(unsigned int) * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int mh_debug_decisions(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decide), sizeof(unsigned long long) * 4) ==
+                   hipSuccess ? 0 : -1;
 }
 #endif
 

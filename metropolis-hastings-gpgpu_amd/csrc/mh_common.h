@@ -24,6 +24,14 @@
 #if MH_CHECK
 static __device__ unsigned int g_check[8];  // (per translation unit) [0] violations, [1] site,
                                             // [2] [3] values, [4] wave, [5] checks made
+static __device__ unsigned long long g_decide[4];  // steps that evaluated the bound, certain
+                                                   // rejects, certain accepts, exact passes of
+                                                   // the current configuration
+__device__ __forceinline__ void mh_count_decision(int d, bool evaluated) {
+    if (evaluated) atomicAdd(&g_decide[0], 1ull);
+    if (d == 1) atomicAdd(&g_decide[1], 1ull);
+    if (d == 2) atomicAdd(&g_decide[2], 1ull);
+}
 __device__ __forceinline__ bool mh_check_fail(unsigned site, unsigned v0, unsigned v1) {
     if (atomicAdd(&g_check[0], 1u) == 0u) {
         g_check[1] = site;
@@ -846,8 +854,10 @@ enum { BOUND_OPEN = 0, BOUND_REJECT = 1, BOUND_ACCEPT = 2 };
 // and this estimate's), each composition step of Costs() (the e1, e2 and 12 U terms), and the
 // roundings no term covers -- the reference's five float additions of the total (:547), each
 // at most U times a partial sum of the components, whose magnitudes add up to at most cabs
-// below; the two additions forming t; and the decision's own arithmetic on t, e and cur (t +
-// 1.25 e, minus cur, the star ends): 8 U cabs + 3 U (|t| + |cur|) covers them.
+// below; the two additions forming t; the weight products' second rounding (e1 and e2 count
+// three of the four roundings of W * component on either side); and the decision's own
+// arithmetic on t, e and cur (t + 1.25 e, minus cur, the star ends): 8 U cabs + 3 U (|o1| +
+// |o2|) + 3 U (|t| + |cur|) covers them.
 template <bool DPW = false>
 __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
                                             const BoundTerms& bt, float u, CostIv cur,
@@ -873,10 +883,12 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const float elin = (26.0f + kf + eacc) * U * afp + (26.0f + kf) * U * fabsf(lsym) +
                        U * wsym + (26.0f + (float)bt.kcl) * U * fabsf(lcl) + U * wcl +
                        (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) + 12.0f * U * alin;
-    // sum[6] bounds sum |area x| and sum |area y| for VisualBalance, and the components' sum
-    // of magnitudes (alin) for the catch-all term
-    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin, bt.anx + bt.any + alin,
-                           bt.aang};
+    // sum[6] bounds sum |area x| and sum |area y| for VisualBalance; the components' sum of
+    // magnitudes (alin, for the catch-all term) rides along in sum[7] with the angle terms'
+    // magnitudes when their sum is fp64 (DPW: sum[7] then only scales a 2^-53 error), in sum[6]
+    // otherwise
+    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin,
+                           bt.anx + bt.any + (DPW ? 0.0f : alin), bt.aang + (DPW ? alin : 0.0f)};
     float sum[8];
     wave_fsum8(part, sum);
     const float s_nx = sum[0], s_ny = sum[1], s_lin = sum[4], s_elin = sum[5];
@@ -920,8 +932,8 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     // total (Kernel.cu:547) and its ends
     const float t = (o1 + o2) + s_lin;
     const float acur = fmaxf(fabsf(cur.lo), fabsf(cur.hi));
-    const float cabs = fabsf(o1) + e1 + fabsf(o2) + e2 + sum[6];
-    const float e = slack * (e1 + e2 + s_elin + 12.0f * U * (fabsf(o1) + e1 + fabsf(o2) + e2) +
+    const float cabs = fabsf(o1) + e1 + fabsf(o2) + e2 + (DPW ? sum[7] : sum[6]);
+    const float e = slack * (e1 + e2 + s_elin + 3.0f * U * (fabsf(o1) + fabsf(o2)) +
                              8.0f * U * cabs + 3.0f * U * (fabsf(t) + acur));
     const float x = (float)kBeta * ((t + 1.25f * e) - cur.lo);   // beta (star - cur), upper end
     const float xl = (float)kBeta * ((t - 1.25f * e) - cur.hi);  // and lower end
@@ -1067,6 +1079,25 @@ __device__ __forceinline__ float accept_threshold(double x) {
     if (x >= 0.0) return 1.0f;
     if (x < -24.0) return 0.0f;
     return fminf(1.0f, (float)exp(x));
+}
+
+// Accept's decision with the proposal's exact total `star` and the current total known only as
+// the interval `cur` (after a proposal accepted on the bound): the threshold min(1, (float)exp(
+// beta (star - cur))) does not increase with cur (the double difference of two floats is
+// exact), so the decision is certain when u lies on one side of the thresholds at both ends --
+// one float ulp apart from them, for the rounding of exp; 1 and 0 are exact. Then no exact pass
+// of the current configuration is needed: BOUND_REJECT, BOUND_ACCEPT or BOUND_OPEN.
+__device__ __forceinline__ int decide_exact_star(float star, CostIv cur, float u, double beta) {
+    const float th_max = accept_threshold(beta * ((double)star - (double)cur.lo));
+    const float th_min = accept_threshold(beta * ((double)star - (double)cur.hi));
+    // (the next float up, for the non-negative finite u and thresholds)
+    auto up = [](float v) { return __uint_as_float(__float_as_uint(v) + 1u); };
+    int d = BOUND_OPEN;
+    if (th_max == 0.0f ? u > 0.0f : u > up(th_max))
+        d = BOUND_REJECT;
+    else if (th_min == 1.0f ? u < 1.0f : up(u) < th_min)
+        d = BOUND_ACCEPT;
+    return __builtin_amdgcn_readfirstlane(d);
 }
 
 template <class Rng>

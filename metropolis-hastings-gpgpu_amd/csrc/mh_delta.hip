@@ -1141,6 +1141,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         }
 #endif
 #if MH_CHECK
+        if (FASTD && r == 0) mh_count_decision(bd, it + 1 < a.iterations);
         // Check builds verify every decision the bound takes against the exact costs (the
         // replay of the lists just built): the proposal's exact total lies in the bound's
         // interval, the current total in the carried one, a certain REJECT / ACCEPT is Accept's.
@@ -1166,6 +1167,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 #endif
         float sc[8];
         bool rare = false;  // the exact pass of the current configuration ran (below)
+        int bd2 = BOUND_OPEN;  // an open step decided by its exact total against the interval
         if (bd == BOUND_OPEN) {
 #if MH_STAMPS > 1
         if (r == 0) {
@@ -1195,8 +1197,11 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
                 for (int k = 0; k < 8; ++k) cur[k] = uniform_f(ro[k]);
                 cur_total = cur[0];
 #if MH_CHECK
-                if (r == 0) MH_CK(cur_total == chk_cur, 24, __float_as_uint(cur_total),
-                                  __float_as_uint(chk_cur));
+                if (r == 0) {
+                    MH_CK(cur_total == chk_cur, 24, __float_as_uint(cur_total),
+                          __float_as_uint(chk_cur));
+                    atomicAdd(&g_decide[3], 1ull);
+                }
 #endif
                 cur_exact = true;
                 cur_iv = CostIv{cur_total, cur_total};
@@ -1205,6 +1210,19 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 #pragma unroll
             for (int k = 0; k < 8; ++k) sc[k] = uniform_f(ro[k]);  // (scalar registers)
             if (!FASTD || cur_exact) break;
+            // The proposal's exact total often decides against the current total's interval
+            // alone (decide_exact_star): then no exact pass of the current configuration. (Not
+            // on a launch's last step: a rejection would leave the current costs inexact, and a
+            // launch ends with them exact.)
+            if (it + 1 < a.iterations) bd2 = decide_exact_star(sc[0], cur_iv, u_acc, kBeta);
+#if MH_CHECK
+            if (r == 0 && bd2 != BOUND_OPEN) {
+                const bool acc_x = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)chk_cur));
+                MH_CK(acc_x == (bd2 == BOUND_ACCEPT), 25, __float_as_uint(sc[0]),
+                      __float_as_uint(chk_cur));
+            }
+#endif
+            if (bd2 != BOUND_OPEN) break;
             // The decision needs the current configuration's exact costs: undo the proposal.
             // The undo records are swapped to its objects' poses and FocalPoint terms (and SAMB
             // keeps its SurfaceArea bits), so a second undo_proposal() re-applies it.
@@ -1237,6 +1255,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         bool acc;
         if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
         else if (bd != BOUND_OPEN) acc = bd == BOUND_ACCEPT;
+        else if (bd2 != BOUND_OPEN) acc = bd2 == BOUND_ACCEPT;
         else acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
         // A rejected proposal is undone; after the exact pass of the current configuration
         // (rare) the state is the current one, and an accepted proposal is re-applied.
@@ -1271,6 +1290,10 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         for (int k = 0; k < 8; ++k) atomicAdd(&g_delta_cycles[k], cyc[k]);
 #endif
 
+#if MH_CHECK
+    if (!TRACK && r == 0)  // a launch ends with the current configuration's exact costs
+        MH_CK(cur[0] == chk_cur, 26, __float_as_uint(cur[0]), __float_as_uint(chk_cur));
+#endif
     if (writer) {
         ChainMeta m;
         m.draws = rng.draws;
@@ -1315,6 +1338,11 @@ hipError_t launch_delta_s(const LaunchArgs& a, int waves_per_wg, hipStream_t str
 extern "C" __attribute__((visibility("default"))) int mh_debug_check_delta(unsigned int* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check), sizeof(unsigned int) * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int mh_debug_decisions_delta(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decide), sizeof(unsigned long long) * 4) ==
+                   hipSuccess ? 0 : -1;
 }
 #endif
 

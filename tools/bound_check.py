@@ -16,7 +16,9 @@ LIB = ROOT / "metropolis-hastings-gpgpu_amd" / "libmhgpu_check.so"  # (__graft_e
 SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept rejects",
          22: "exact total outside the bound's interval",
          23: "current total outside the carried interval",
-         24: "exact pass of the current configuration differs from the carried total"}
+         24: "exact pass of the current configuration differs from the carried total",
+         25: "exact total against the current interval decided wrongly",
+         26: "a launch ended without the current configuration's exact costs"}
 
 # (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
 # object far outside the proven symmetry range, "negw" flips the weights' signs.
@@ -63,10 +65,17 @@ def one(kind, n, chains, steps, kernel):
     ck = (C.c_uint * 8)()
     fn = lib.mh_debug_check_delta if kernel == "incremental" else lib.mh_debug_check
     assert fn(ck) == 0
+    dc = (C.c_ulonglong * 4)()
+    fd = lib.mh_debug_decisions_delta if kernel == "incremental" else lib.mh_debug_decisions
+    assert fd(dc) == 0
+    steps_all = float(chains * steps)
+    rates = (f"; of {chains * steps} steps: certain reject {dc[1] / steps_all:.4f}, certain "
+             f"accept {dc[2] / steps_all:.4f}, open {(dc[0] - dc[1] - dc[2]) / steps_all:.4f}, "
+             f"exact current pass {dc[3] / steps_all:.4f}") if dc[0] else ""
     site = SITES.get(ck[1], str(ck[1]))
     print(f"[bound] {kind} N={n} {kernel}: {chains} x {steps} steps, {ck[5]} bound decisions "
           f"checked, violations {ck[0]}" + (f" (first: {site}, values {ck[2]:#x} {ck[3]:#x})"
-                                            if ck[0] else ""), flush=True)
+                                            if ck[0] else "") + rates, flush=True)
     return ck[0] == 0
 
 
