@@ -187,6 +187,90 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
     rel_terms(ch.relc[q], ch.P, tpw, tang);
 }
 
+// ---- FocalPoint and relationship terms of one lane, exact or estimated ------------------------
+//
+// Steps with one object per lane: lane i holds object i's FocalPoint term and relationship i's
+// PairWise / PairWiseAngle terms. exact_terms() evaluates them as the reference does (double
+// atan2, double cos rounded to float, double distance and divisions, Kernel.cu:170-188,
+// 210-281); one shared atan2 pass serves a lane's relationship or, failing that, its object, and
+// a lane that needs both takes a second (rare) pass.
+__device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
+                                            bool obj, bool rel, float& cph, double& rpw,
+                                            double& rang) {
+    const ObjP p = ch.P[i < n ? i : 0];
+    const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
+    double dy = fy, dx = fx, tpw = 0.0;
+    float ti = 0.0f;
+    if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
+    double a1 = 0.0, a2 = 0.0;
+    if (rel || obj) a1 = atan2(dy, dx);
+    if (rel && obj) a2 = atan2(fy, fx);
+    if (obj) {
+        const float at = (float)(rel ? a2 : a1);
+        const float b = at - p.rotYf;
+        const float ph = (float)((double)b + kHalfPI);
+        cph = cos_f32(ph);
+    }
+    if (rel) {
+        rpw = tpw;
+        rang = rel_angle(ch.relc[i], a1, ti);
+    }
+}
+
+// fp32 estimates of the same terms for the rejection bound (no double transcendental): cph
+// within kDeltaCph, rpw within 12 U relative, rang within eang (returned). `amb` is set where the
+// estimate lies too near one of the reference's discontinuities for its branch to be certain --
+// the distance range's ends (:216-221), theta's two wraps (:176-181), the wrapped range's fmodf
+// and switch (:245-250) -- or the range normaliser is degenerate; such a lane needs exact_terms().
+__device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
+                                             bool obj, bool rel, float& cph, double& rpw,
+                                             double& rang, float& eang, bool& amb) {
+    constexpr float U = 0x1p-24f;
+    if (obj) {
+        const ObjP p = ch.P[i < n ? i : 0];
+        const float at = atan2f(rm.fyf - p.yf, rm.fxf - p.xf);
+        const float b = at - p.rotYf;
+        cph = cosf(b + (float)kHalfPI);
+    }
+    if (rel) {
+        const RelConst& rc = ch.relc[i];
+        const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
+        const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;  // (the reference's float differences)
+        const float d = __builtin_sqrtf(fx * fx + fy * fy);   // within 2 U of its double distance
+        const float st = (float)rc.start, en = (float)rc.end;
+        amb |= fabsf(d - st) <= 8.0f * U * fabsf(st) || fabsf(d - en) <= 8.0f * U * fabsf(en);
+        float f = 0.0f;
+        if (d < st) f = d / st;
+        else if (d > en) f = en / d;
+        rpw = (double)(f * f);
+        const ObjP as = ch.P[rc.as], atp = ch.P[rc.at];
+        const float dxa = as.xf - atp.xf, dya = as.yf - atp.yf;
+        float tp = atan2f(dya, dxa);
+        amb |= fabsf(tp) <= kDeltaTh && !(dxa == 0.0f && dya == 0.0f);
+        if (tp < 0.0f) tp = tp + (float)kTwoPI;
+        const float t = tp - atp.rotYf;
+        amb |= fabsf(t) <= kDeltaTh;
+        const float th = t < 0.0f ? t + (float)kTwoPI : t;
+        bool on;
+        double norm;
+        if (rc.amin > rc.amax) {
+            const float w = fmodf((float)(rc.amin + (double)th), (float)kTwoPI);
+            amb |= fabsf(w - (float)rc.amax) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
+                   fabsf(w - (float)kTwoPI) <= 2.0f * kDeltaTh;
+            on = (double)w > rc.amax;
+            norm = rc.norm_w;
+        } else {
+            on = rc.amin < (double)th || (double)th < rc.amax;  // (continuous at its switch)
+            norm = rc.norm_n;
+        }
+        amb |= !(fabs(norm) >= 1e-3);
+        const double v = on ? fmin(fabs((double)th - rc.amin), fabs((double)th - rc.amax)) / norm
+                            : 0.0;
+        rang = v;
+        eang = (float)((double)(2.0f * kDeltaTh) / fabs(norm)) + 4.0f * U * (float)fabs(v);
+    }
+}
+
 // ---- incremental Clearance pairs (one object per lane) ---------------------------------------
 //
 // A proposal changes the pairs of the moved objects' columns and of the rows of clearances they
@@ -297,39 +381,43 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         sao[m] = sac[m] = boxo[m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (SHARED) {
             // Steps, one object per lane: only the moved objects' FocalPoint terms and the
-            // relationships they touch change; the rest keep their terms. Both need an atan2
-            // (phi, Kernel.cu:187; theta, :175): one shared pass serves a lane's relationship
-            // or, failing that, its object; a lane that needs both takes a second (rare) pass.
-            // (It runs first, so the per-object values below are not live across the atan2.)
-            const bool obj = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
-            bool rel = false;
+            // relationships they touch change; the rest keep their terms (clp). Steps that
+            // decide on the rejection bound (FAST) take fp32 estimates of the changed terms and
+            // mark them (dc, dr); exact passes evaluate every marked or changed term exactly.
+            // (This runs first, so the per-object values below are not live across the atan2.)
+            const bool moved = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
+            bool touched = false;
             if (i < rm.r && !(MH_ABLATE & 16)) {
                 const RelConst& rc = ch.relc[i];
-                rel = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka || rc.at == ka ||
-                                  rc.s == kb || rc.t == kb || rc.as == kb || rc.at == kb);
+                touched = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka || rc.at == ka ||
+                                      rc.s == kb || rc.t == kb || rc.as == kb || rc.at == kb);
             }
-            const ObjP p = ch.P[i < n ? i : 0];
-            const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
-            double dy = fy, dx = fx, tpw = 0.0;
-            float ti = 0.0f;
-            if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
-            double a1 = 0.0, a2 = 0.0;
-            if (rel || obj) a1 = atan2(dy, dx);
-            if (rel && obj) a2 = atan2(fy, fx);
-            if (obj) {
-                float at = (float)(rel ? a2 : a1);
-                float b = at - p.rotYf;
-                float ph = (float)((double)b + kHalfPI);
-                cph[m] = cos_f32(ph);
+            cph[m] = clp.cph;
+            rpw[m] = clp.rpw;
+            rang[m] = clp.rang;
+            clo.dc = clp.dc;
+            clo.dr = clp.dr;
+            clo.eang = clp.eang;
+            if constexpr (FAST) {
+                bool amb = false;
+                if (__ballot(moved || touched))
+                    approx_terms(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
+                                 amb);
+                clo.dc = clo.dc || moved;
+                clo.dr = clo.dr || touched;
+                if (__ballot(amb)) {  // (rare) an estimate near a discontinuity: exact instead
+                    if (amb) {
+                        clo.dr = false;
+                        clo.eang = 0.0f;
+                    }
+                    exact_terms(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
+                }
             } else {
-                cph[m] = clp.cph;
-            }
-            if (rel) {
-                rpw[m] = tpw;
-                rang[m] = rel_angle(ch.relc[i], a1, ti);
-            } else {
-                rpw[m] = clp.rpw;
-                rang[m] = clp.rang;
+                const bool obj = moved || (i < n && clp.dc);
+                const bool rel = touched || (i < rm.r && clp.dr);
+                if (__ballot(obj || rel)) exact_terms(ch, rm, i, n, obj, rel, cph[m], rpw[m], rang[m]);
+                clo.dc = clo.dr = false;
+                clo.eang = 0.0f;
             }
         }
         if (i < n) {
@@ -371,6 +459,10 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             clo.rpw = rpw[0];
             clo.rang = rang[0];
             clo.cph = cph[0];
+            if constexpr (!SHARED) {
+                clo.dc = clo.dr = false;
+                clo.eang = 0.0f;
+            }
         }
         if (i < c) {
             const RectShape cs = ch.clrs[i];
@@ -689,6 +781,9 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             bt.kcl = kcl;
             bt.clpos = 0.0f;  // (no position credit: the list positions are not formed here)
             bt.pwd = bt.angd = 0.0;
+            bt.efp = r < n && clo.dc ? kDeltaCph : 0.0f;  // (fp32 estimates, approx_terms)
+            bt.eang = r < rm.r && clo.dr ? clo.eang : 0.0f;
+            bt.pwx = __ballot(r < rm.r && clo.dr) ? 12 : 0;
             bt.sa = -((sac[0].x + sac[0].y + sac[0].z + sac[0].w) +
                       (sao[0].x + sao[0].y + sao[0].z + sao[0].w));
             bt.pw = -(float)rpw[0];
@@ -709,6 +804,30 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                 *fast = d;
                 return;
             }
+            // The exact sums are needed: every estimated term is made exact first.
+            const bool obj = r < n && clo.dc, rel = r < rm.r && clo.dr;
+            if (__ballot(obj || rel)) {
+                float c0 = cph[0];
+                double p0 = rpw[0], a0 = rang[0];
+                exact_terms(ch, rm, r, n, obj, rel, c0, p0, a0);
+#if MH_CHECK
+                // the estimates' allowances, against the exact values
+                MH_CK(!obj || fabsf(cph[0] - c0) <= kDeltaCph, 30, __float_as_uint(cph[0]),
+                      __float_as_uint(c0));
+                MH_CK(!rel || fabs(rpw[0] - p0) <= 12.0 * 0x1p-24 * fabs(p0) + 1e-30, 31,
+                      __float_as_uint((float)rpw[0]), __float_as_uint((float)p0));
+                MH_CK(!rel || fabs(rang[0] - a0) <= (double)clo.eang, 32,
+                      __float_as_uint((float)rang[0]), __float_as_uint((float)a0));
+#endif
+                cph[0] = c0;
+                rpw[0] = p0;
+                rang[0] = a0;
+                clo.cph = c0;
+                clo.rpw = p0;
+                clo.rang = a0;
+            }
+            clo.dc = clo.dr = false;
+            clo.eang = 0.0f;
         }
     }
     // The eight ordered sums of Costs() -- VisualBalance nx and ny (float through double

@@ -748,6 +748,9 @@ struct BoundTerms {
     float pw, ang, aang;     // PairWise -(range term) (<= 0), PairWiseAngle (:222, :249-253)
     double pwd, angd;        // the same PairWise / PairWiseAngle partial sums in double
                              // (bound_decide<true>: the two sums in fp64)
+    float efp;               // absolute error of this lane's FocalPoint terms (fp32 estimates)
+    float eang;              // absolute error of this lane's PairWiseAngle terms (estimates)
+    int pwx;                 // relative error of estimated PairWise terms, in U (uniform)
     int k;                   // most terms any lane pre-sums into any other partial sum (the
                              // same value on every lane: it enters the uniform bound)
 };
@@ -882,13 +885,18 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const float wcl = fabsf(rm.w_cl) * fmaxf(0.0f, (float)ncl * fabsf(bt.cl) - bt.clpos);
     const float elin = (26.0f + kf + eacc) * U * afp + (26.0f + kf) * U * fabsf(lsym) +
                        U * wsym + (26.0f + (float)bt.kcl) * U * fabsf(lcl) + U * wcl +
-                       (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) + 12.0f * U * alin;
+                       (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) + 12.0f * U * alin +
+                       fabsf(rm.w_fp) * bt.efp;
+    // (fp32 path: the PairWise sum's relative allowance, estimates included; the angle terms'
+    // absolute allowances enter its magnitude sum scaled by 1 / cr, so eang = cr a_ang covers them)
+    const float cr32 = (26.0f + kf + eacc + (float)bt.pwx) * U;
     // sum[6] bounds sum |area x| and sum |area y| for VisualBalance; the components' sum of
     // magnitudes (alin, for the catch-all term) rides along in sum[7] with the angle terms'
     // magnitudes when their sum is fp64 (DPW: sum[7] then only scales a 2^-53 error), in sum[6]
     // otherwise
     const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin,
-                           bt.anx + bt.any + (DPW ? 0.0f : alin), bt.aang + (DPW ? alin : 0.0f)};
+                           bt.anx + bt.any + (DPW ? 0.0f : alin),
+                           bt.aang + (DPW ? alin : bt.eang / cr32)};
     float sum[8];
     wave_fsum8(part, sum);
     const float s_nx = sum[0], s_ny = sum[1], s_lin = sum[4], s_elin = sum[5];
@@ -922,8 +930,7 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
               (float)(0x1p-52 * fabs(pad));
     } else {
         const float s_pw = sum[2], s_ang = sum[3];
-        const float cr = (26.0f + kf + eacc) * U;  // (double accumulators)
-        const float epw = cr * fabsf(s_pw), eang = cr * a_ang;
+        const float epw = cr32 * fabsf(s_pw), eang = cr32 * a_ang;  // (double accumulators)
         pa = s_pw * s_ang;
         dpa = fabsf(s_pw) * eang + fabsf(s_ang) * epw + epw * eang;
     }
@@ -979,7 +986,19 @@ struct ClPairs {
     double rpw, rang;  // this lane's relationship terms (kept for relationships a move misses)
     float cph;         // this lane's object's cos(phi) (kept for objects a move misses)
     float4 sac;        // SurfaceArea overlaps of clearance `lane` at object `lane`'s pose
+    bool dc, dr;       // cph / rpw, rang hold fp32 estimates, not the reference's values (steps
+                       // the rejection bound decides compute only those; an exact pass fixes
+                       // them when a step needs the exact sums)
+    float eang;        // the allowance of an estimated rang
 };
+
+// Allowances of the fp32 estimates of the FocalPoint and relationship terms (mh_chain.hip
+// approx_terms): |cos(phi) estimate - the reference's float| <= kDeltaCph, theta's estimate
+// within kDeltaTh of the reference's double, the PairWise term within 12 U relative. The
+// derivation assumes fp32 atan2 and cos within 4 ulp (OCML's are within 2-3); the check build
+// verifies every estimate against the exact value.
+constexpr float kDeltaCph = 0x1p-17f;
+constexpr float kDeltaTh = 0x1p-17f;
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
 // Split form for callers that batch the atan2: rel_pair() gives the PairWise term and theta's
