@@ -367,11 +367,14 @@ __device__ __forceinline__ void nz_row(const DeltaPtrs& ch, Own<S>& o, int n, in
 }
 
 // Clearance boxes and pair bits after objects ka, kb changed (also restores them after a
-// rejected proposal has put the old poses back).
+// rejected proposal has put the old poses back). Returns whether this lane's first row
+// (clearance r < 64) may have changed: its clearance moved, or it pairs with ka or kb before or
+// after (the row's cached sums, ClRow, must then be recomputed).
 template <int S>
-__device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, int n, int c,
+__device__ __forceinline__ bool clearance_delta(const DeltaPtrs& ch, Own<S>& o, int n, int c,
                                                 int ka, int kb, int r) {
-    if (ka < 0 && kb < 0) return;
+    if (ka < 0 && kb < 0) return false;
+    bool chg0 = false;
     uint64_t rows = 0;
     int t = 0;
     for (int ci = r; ci < c; ci += L, ++t) {
@@ -381,6 +384,7 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
             rows |= 1ull << t;
         }
     }
+    chg0 = (rows & 1ull) != 0;  // (a moved row is rebuilt below)
     wave_sync();
     // Columns ka, kb of the rows whose clearance did not move (lane-owned rows).
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -394,6 +398,7 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
             const bool nz = overlap(cla_get<S>(ch, o, ci), bj) != 0.0f;
             if (t == 0) {
                 const uint64_t w0 = o.nz0[j >> 6];
+                chg0 = chg0 || nz || (w0 & bit) != 0;
                 o.nz0[j >> 6] = nz ? (w0 | bit) : (w0 & ~bit);
             } else {
                 uint64_t* wd = &ch.NZ[(ci - 64) * S + (j >> 6)];
@@ -410,6 +415,7 @@ __device__ __forceinline__ void clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
         nz_row<S>(ch, o, n, tb * L + b, r);
         if (r == b) rows &= rows - 1;
     }
+    return chg0;
 }
 
 // PairWise / PairWiseAngle terms of the relationships touching ka or kb (or all, ka = -2).
@@ -439,6 +445,39 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
 }
 
 // ---- compacted Clearance / SurfaceArea terms ------------------------------------------------
+
+// The rejection bound's Clearance terms of this lane's first row (clearance r < 64): their
+// negated sum in the row's order, their count, and the sum of in-row position x |term|. Kept per
+// configuration and recomputed only for rows a proposal may change (clearance_delta), so a step
+// the bound decides builds no Clearance list. (Rooms of more than 64 clearances use the list
+// build for the bound, as the rows past 64 are not cached.)
+struct ClRow {
+    float sum;
+    int cnt;
+    float pos;
+};
+
+template <int S>
+__device__ __forceinline__ ClRow cl_row0(const DeltaPtrs& ch, const Own<S>& o, int c, int r,
+                                         bool active) {
+    ClRow w{0.0f, 0, 0.0f};
+    if (active && r < c) {
+        const float4 A = o.cla0;
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            uint64_t word = o.nz0[q];
+            while (word) {
+                const int j = q * 64 + __builtin_ctzll(word);
+                word &= word - 1;
+                const float v = -overlap(A, obj_box(ch, j));
+                w.sum += v;
+                w.pos = fmaf((float)w.cnt, -v, w.pos);
+                ++w.cnt;
+            }
+        }
+    }
+    return w;
+}
 
 // Non-zero Clearance terms, clearance-major then object (Kernel.cu:408-431), negated: those at
 // positions [lo, lo + cap_cl) go to LCL[pos - lo]. Returns the total count. With `sum`, also
@@ -1044,6 +1083,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     for (int ci = r; ci < c; ci += L) cla_put<S>(ch, o, ci, cla_box(ch, ci));
     wave_sync();
     for (int ci = 0; ci < c; ++ci) nz_row<S>(ch, o, n, ci, r);
+    ClRow rc_cur = cl_row0<S>(ch, o, c, r, true);  // (the current configuration's first rows)
     rels_delta(ch, nr, -2, -1, r);
     for (int i = 0; i < n; ++i) {
         const RowMax s = scan_row<S>(ch, o, n, i, wild_cnt > 0, r);
@@ -1104,7 +1144,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         const int wild_star = wild_cnt + __shfl(dwild, 0) + __shfl(dwild, 1);
         wave_sync();
         DSTAMP(0);
-        clearance_delta<S>(ch, o, n, c, ka, kb, r);
+        const bool chg0 = clearance_delta<S>(ch, o, n, c, ka, kb, r);
         DSTAMP(1);
         rels_delta(ch, nr, ka, kb, r);
         DSTAMP(2);
@@ -1119,8 +1159,34 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         CostIv star_iv{0.0f, 0.0f};
         float u_acc = 0.0f;
         float clsum = 0.0f, sasum = 0.0f, clpos = 0.0f;
-        int kcl = 0;
-        const int cnt_cl = build_cl_list<S>(ch, o, c, r, 0, &clsum, &kcl, &clpos);
+        int kcl = 0, cnt_cl = 0;
+        bool cl_built = false;  // (the Clearance list for the replay is written)
+        ClRow rc_star = rc_cur;  // the proposal's first-row Clearance sums
+        if (FASTD && c <= 64) {
+            const ClRow f = cl_row0<S>(ch, o, c, r, chg0);
+            if (chg0) rc_star = f;
+            const int cnt = r < c ? rc_star.cnt : 0;
+            const int base0 = group_excl_scan<L>(cnt, r, cnt_cl);
+            if (r < c) {
+                clsum = rc_star.sum;
+                kcl = cnt;
+                clpos = fmaf((float)base0, -rc_star.sum, rc_star.pos);
+            }
+        } else {
+            cnt_cl = build_cl_list<S>(ch, o, c, r, 0, &clsum, &kcl, &clpos);
+            cl_built = true;
+        }
+#if MH_CHECK
+        if (!cl_built) {  // the cached row sums against a fresh build
+            float cs = 0.0f, cp = 0.0f;
+            int kc = 0;
+            const int cn = build_cl_list<S>(ch, o, c, r, 0, &cs, &kc, &cp);
+            MH_CK(cs == clsum && kc == kcl && cn == cnt_cl &&
+                      fabsf(cp - clpos) <= 1e-5f * fabsf(cp) + 1e-30f,
+                  27, __float_as_uint(cs), __float_as_uint(clsum));
+            cl_built = true;
+        }
+#endif
         const int cnt_sa = build_sa_list(ch, n, c, r, 0, &sasum);
         if constexpr (FASTD) {
             u_acc = rng.uniform();
@@ -1179,6 +1245,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             atomicAdd(&g_delta_counts[3], (unsigned long long)(cnt_sa > ch.cap_sa));
         }
 #endif
+        if (!cl_built) build_cl_list<S>(ch, o, c, r, 0);
         DSTAMP(4);
         // Pass 0 replays the proposal's sums. When the current total is only an interval
         // (FASTD, cur_exact false), pass 1 undoes the proposal and replays the current
@@ -1267,6 +1334,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 #if MH_CHECK
             chk_cur = bd == BOUND_OPEN ? sc[0] : chk_star;
 #endif
+            rc_cur = rc_star;
             o.cmx = o.pmx;
             o.carg = o.parg;
             wild_cnt = wild_star;
