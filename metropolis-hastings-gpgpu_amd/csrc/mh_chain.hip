@@ -280,7 +280,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
 template <int L>
 __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, int ka, int kb,
                                              int r, int gbase, float4 boxj, const ClPairs& clp,
-                                             ClPairs& clo) {
+                                             ClPairs& clo, bool& colchg) {
     const int j = r;
     const uint64_t* NZc = ch.NZ + clp.buf * c;
     uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
@@ -306,6 +306,7 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
         moved &= moved - 1;
         const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
         const uint64_t row = group_ballot<L>(nzi, gbase);
+        colchg = colchg || nzi || ((cm >> i) & 1ull) != 0;  // (the pair before or after)
         cm = (cm & ~(1ull << i)) | ((uint64_t)nzi << i);
         if (r == i) w = row;
     }
@@ -755,19 +756,43 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // clearances its latency is lower, and those rooms run few chains).
     constexpr bool INC_CL = DELTA && NPL == 1 && L >= 16;
     int cl_total = 0;
-    if constexpr (INC_CL) cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo);
+    // (a lane's column of Clearance pairs changes when its object moved or a moved clearance
+    // pairs with it before or after)
+    bool colchg = r < n && (r == ka || r == kb);
+    if constexpr (INC_CL)
+        cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo, colchg);
     if (r == 0) MH_PHASE(ch, 3, t0);
     if constexpr (FAST) {
         static_assert(INC_CL && L == 64, "the rejection bound needs one chain per wavefront");
         if (rm.r <= L) {  // every relationship term is held by a lane (rpw[0], rang[0])
-            float clsum = 0.0f;  // this lane's object against the clearances it overlaps
+            // this lane's object against the clearances it overlaps: kept from the current
+            // configuration unless its column may have changed
+            float clsum = clp.clc;
             uint64_t bits = r < n ? clo.cm : 0ull;
             const int kcl = __builtin_popcountll(bits);
-            while (bits) {
-                const int i = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                clsum += overlap(ch.CLA[i], boxo[0]);
+            if (__ballot(colchg)) {
+                if (colchg) {
+                    clsum = 0.0f;
+                    while (bits) {
+                        const int i = __builtin_ctzll(bits);
+                        bits &= bits - 1;
+                        clsum += overlap(ch.CLA[i], boxo[0]);
+                    }
+                }
             }
+            clo.clc = clsum;
+#if MH_CHECK
+            {  // the cached column sum against a fresh one
+                float f = 0.0f;
+                uint64_t b2 = r < n ? clo.cm : 0ull;
+                while (b2) {
+                    const int i = __builtin_ctzll(b2);
+                    b2 &= b2 - 1;
+                    f += overlap(ch.CLA[i], boxo[0]);
+                }
+                MH_CK(f == clsum, 28, __float_as_uint(f), __float_as_uint(clsum));
+            }
+#endif
             BoundTerms bt;
             bt.nx = (float)px[0];
             bt.ny = (float)py[0];
@@ -892,14 +917,18 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         } else if constexpr (!DELTA && CL_STATE) {
             // full evaluation: the pair state from scratch, for the steps that follow
             uint64_t cm = 0ull;
+            float clc = 0.0f;
             for (int i = 0; i < c; ++i) {
-                const bool nzi = j < n && overlap(ch.CLA[i], boxj) != 0.0f;
+                const float ov = j < n ? overlap(ch.CLA[i], boxj) : 0.0f;
+                const bool nzi = ov != 0.0f;
                 const uint64_t row = group_ballot<L>(nzi, gbase);
                 cm |= (uint64_t)nzi << i;
+                if (nzi) clc += ov;
                 if (r == 0) ch.NZ[i] = row;
             }
             clo.cm = cm;
             clo.buf = 0;
+            clo.clc = clc;
         }
     }
     for (int rep = 0; rep < MH_REPS(8); ++rep) {

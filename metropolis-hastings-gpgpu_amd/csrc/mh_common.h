@@ -990,6 +990,8 @@ struct ClPairs {
                        // the rejection bound decides compute only those; an exact pass fixes
                        // them when a step needs the exact sums)
     float eang;        // the allowance of an estimated rang
+    float clc;         // the rejection bound's Clearance partial sum of this lane's object
+                       // (its column, clearances in order): recomputed only when it may change
 };
 
 // Allowances of the fp32 estimates of the FocalPoint and relationship terms (mh_chain.hip
