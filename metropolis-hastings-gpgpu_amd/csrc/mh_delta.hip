@@ -70,6 +70,11 @@ struct Own {
     ivec parg;
     wvec nz0;  // the non-zero Clearance pair words of clearance r (rows >= 64 live in LDS)
     float4 cla0;  // clearance r's box at its source object (clearances >= 64: LDS)
+    // SurfaceArea entry e = 64 t + r (t < 2S: C + N <= 128 S) of the current configuration, as
+    // the rejection bound sums it: (v.x + v.y) + (v.z + v.w) of its four overlaps (zero when
+    // they all are), so a step the bound decides builds no SurfaceArea list
+    typedef float svec __attribute__((ext_vector_type(2 * S)));
+    svec sav;
 };
 
 // v[m] = x where pred holds (m may differ between lanes).
@@ -1078,8 +1083,18 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         }
     }
     int wild_cnt = group_sum<L>(wild);
-    for (int e = r; e < c + n; e += L)
-        if (nonzero4(sa_entry(ch, c, e))) sam_put(ch, e, true);
+#pragma unroll
+    for (int t = 0; t < 2 * S; ++t) {
+        const int e = t * L + r;
+        o.sav[t] = 0.0f;
+        if (e < c + n) {
+            const float4 v = sa_entry(ch, c, e);
+            if (nonzero4(v)) {
+                sam_put(ch, e, true);
+                o.sav[t] = (v.x + v.y) + (v.z + v.w);
+            }
+        }
+    }
     for (int ci = r; ci < c; ci += L) cla_put<S>(ch, o, ci, cla_box(ch, ci));
     wave_sync();
     for (int ci = 0; ci < c; ++ci) nz_row<S>(ch, o, n, ci, r);
@@ -1128,14 +1143,20 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         // Objects ka (lane 0) and kb (lane 1): FocalPoint term, SurfaceArea bits, wildness.
         int dwild = 0;
         const double rka = obj_ry<S>(o, ka < 0 ? 0 : ka), rkb = obj_ry<S>(o, kb < 0 ? 0 : kb);
+        float sv_obj = 0.0f, sv_clr = 0.0f;  // (lanes 0, 1: the moved objects' SurfaceArea sums)
         if (r < 2) {
             const int k = r == 0 ? ka : kb;
             if (k >= 0) {
                 const ObjP p = obj_pose(ch, k);
                 ch.CPH[k] = -focal_cos(*rm_l, p.xf, p.yf, p.rotYf);
-                sam_put(ch, c + k, nonzero4(comp_overlaps(*rm_l, ch.BOX[k])));
-                if (k < c)
-                    sam_put(ch, k, nonzero4(comp_overlaps(*rm_l, shape_box(ch.clrs[k], p.xf, p.yf))));
+                const float4 vo = comp_overlaps(*rm_l, ch.BOX[k]);
+                sam_put(ch, c + k, nonzero4(vo));
+                sv_obj = nonzero4(vo) ? (vo.x + vo.y) + (vo.z + vo.w) : 0.0f;
+                if (k < c) {
+                    const float4 vc = comp_overlaps(*rm_l, shape_box(ch.clrs[k], p.xf, p.yf));
+                    sam_put(ch, k, nonzero4(vc));
+                    sv_clr = nonzero4(vc) ? (vc.x + vc.y) + (vc.z + vc.w) : 0.0f;
+                }
                 const DBackup& ob = ch.aux->b[r];
                 dwild = (wild_pose(ch.X[k], ch.Y[k], r == 0 ? rka : rkb) ? 1 : 0) -
                         (wild_pose(ob.x, ob.y, ob.ry) ? 1 : 0);
@@ -1187,7 +1208,35 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             cl_built = true;
         }
 #endif
-        const int cnt_sa = build_sa_list(ch, n, c, r, 0, &sasum);
+        // SurfaceArea: the cached entry sums with the moved objects' entries replaced (lanes 0 and
+        // 1 computed them above); the list itself only for the steps that replay
+        const float sv[4] = {__shfl(sv_obj, 0), __shfl(sv_clr, 0), __shfl(sv_obj, 1),
+                             __shfl(sv_clr, 1)};
+        const int se[4] = {ka >= 0 ? c + ka : -1, ka >= 0 && ka < c ? ka : -1,
+                           kb >= 0 ? c + kb : -1, kb >= 0 && kb < c ? kb : -1};
+        int cnt_sa = 0;
+        bool sa_built = false;
+        if constexpr (FASTD) {
+#pragma unroll
+            for (int t = 0; t < 2 * S; ++t) {
+                const int e = t * L + r;
+                float v = o.sav[t];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v = e == se[q] ? sv[q] : v;
+                sasum -= v;
+            }
+        } else {
+            cnt_sa = build_sa_list(ch, n, c, r, 0, &sasum);
+            sa_built = true;
+        }
+#if MH_CHECK
+        if (!sa_built) {  // the cached entry sums against a fresh build
+            float sf = 0.0f;
+            cnt_sa = build_sa_list(ch, n, c, r, 0, &sf);
+            MH_CK(sf == sasum, 29, __float_as_uint(sf), __float_as_uint(sasum));
+            sa_built = true;
+        }
+#endif
         if constexpr (FASTD) {
             u_acc = rng.uniform();
             BoundTerms bt = delta_bound_terms<S>(ch, o, n, c, nr, r);
@@ -1237,6 +1286,8 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         bool rare = false;  // the exact pass of the current configuration ran (below)
         int bd2 = BOUND_OPEN;  // an open step decided by its exact total against the interval
         if (bd == BOUND_OPEN) {
+        if (!cl_built) build_cl_list<S>(ch, o, c, r, 0);  // (the lists the replay walks)
+        if (!sa_built) cnt_sa = build_sa_list(ch, n, c, r, 0);
 #if MH_STAMPS > 1
         if (r == 0) {
             atomicAdd(&g_delta_counts[0], (unsigned long long)cnt_cl);
@@ -1245,7 +1296,6 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             atomicAdd(&g_delta_counts[3], (unsigned long long)(cnt_sa > ch.cap_sa));
         }
 #endif
-        if (!cl_built) build_cl_list<S>(ch, o, c, r, 0);
         DSTAMP(4);
         // Pass 0 replays the proposal's sums. When the current total is only an interval
         // (FASTD, cur_exact false), pass 1 undoes the proposal and replays the current
@@ -1335,6 +1385,12 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             chk_cur = bd == BOUND_OPEN ? sc[0] : chk_star;
 #endif
             rc_cur = rc_star;
+#pragma unroll
+            for (int t = 0; t < 2 * S; ++t) {  // (the proposal's SurfaceArea entry sums)
+                const int e = t * L + r;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o.sav[t] = e == se[q] ? sv[q] : o.sav[t];
+            }
             o.cmx = o.pmx;
             o.carg = o.parg;
             wild_cnt = wild_star;

@@ -20,7 +20,8 @@ SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept
          25: "exact total against the current interval decided wrongly",
          26: "a launch ended without the current configuration's exact costs",
          27: "cached Clearance row sums differ from a fresh build",
-         28: "cached Clearance column sum differs from a fresh one"}
+         28: "cached Clearance column sum differs from a fresh one",
+         29: "cached SurfaceArea sums differ from a fresh build"}
 
 # (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
 # object far outside the proven symmetry range, "negw" flips the weights' signs.
