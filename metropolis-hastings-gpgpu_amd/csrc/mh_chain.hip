@@ -26,7 +26,8 @@
 #endif
 #ifndef MH_DOUBLE
 #define MH_DOUBLE 0  // cost-probe builds: run phase k twice when bit k is set; product = 0
-                     // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay)
+                     // (1 A, 2 full symmetry, 64 delta symmetry, 4 SA, 8 CL, 16 PW/ANG, 32 replay,
+                     // 128 Clearance pair update, 256 the rejection bound's lane terms and sums)
 #endif
 #define MH_REPS(bit) ((MH_DOUBLE & (bit)) ? 2 : 1)
 #define MH_CLOBBER() asm volatile("" ::: "memory")
@@ -106,6 +107,7 @@ struct ChainPtrs {
     const RectShape* objs;  // room tables, staged once per workgroup into LDS (ChainLds)
     const RectShape* clrs;
     const RelConst* relc;
+    const uint2* rix;  // [R] relationship i's objects {s | t << 16, as | at << 16}
     ObjP* P;
     double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
     double *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
@@ -389,9 +391,12 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const bool moved = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
             bool touched = false;
             if (i < rm.r && !(MH_ABLATE & 16)) {
-                const RelConst& rc = ch.relc[i];
-                touched = ka >= 0 && (rc.s == ka || rc.t == ka || rc.as == ka || rc.at == ka ||
-                                      rc.s == kb || rc.t == kb || rc.as == kb || rc.at == kb);
+                const uint2 q = ch.rix[i];
+                const unsigned a16 = (unsigned)ka, b16 = (unsigned)kb;  // (ka, kb < 65536)
+                touched = ka >= 0 && ((q.x & 0xffffu) == a16 || (q.x >> 16) == a16 ||
+                                      (q.y & 0xffffu) == a16 || (q.y >> 16) == a16 ||
+                                      (q.x & 0xffffu) == b16 || (q.x >> 16) == b16 ||
+                                      (q.y & 0xffffu) == b16 || (q.y >> 16) == b16);
             }
             cph[m] = clp.cph;
             rpw[m] = clp.rpw;
@@ -759,14 +764,33 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // (a lane's column of Clearance pairs changes when its object moved or a moved clearance
     // pairs with it before or after)
     bool colchg = r < n && (r == ka || r == kb);
-    if constexpr (INC_CL)
-        cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo, colchg);
+    if constexpr (INC_CL) {
+#if MH_DOUBLE & 128
+        const bool colchg0 = colchg;
+        for (int rep = 0; rep < 2; ++rep) {
+            MH_CLOBBER();
+            colchg = colchg0;
+#endif
+            cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo, colchg);
+#if MH_DOUBLE & 128
+        }
+#endif
+    }
     if (r == 0) MH_PHASE(ch, 3, t0);
     if constexpr (FAST) {
         static_assert(INC_CL && L == 64, "the rejection bound needs one chain per wavefront");
         if (rm.r <= L) {  // every relationship term is held by a lane (rpw[0], rang[0])
             // this lane's object against the clearances it overlaps: kept from the current
             // configuration unless its column may have changed
+            int d = BOUND_OPEN;
+#if MH_DOUBLE & 256
+            for (int rep = 0; rep < 2; ++rep) {
+            MH_CLOBBER();
+            double px0 = px[0];
+            asm volatile("" : "+v"(px0));  // (the probe's second pass is not folded into the first)
+#else
+            const double px0 = px[0];
+#endif
             float clsum = clp.clc;
             uint64_t bits = r < n ? clo.cm : 0ull;
             const int kcl = __builtin_popcountll(bits);
@@ -794,7 +818,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             }
 #endif
             BoundTerms bt;
-            bt.nx = (float)px[0];
+            bt.nx = (float)px0;
             bt.ny = (float)py[0];
             bt.anx = fabsf(bt.nx);
             bt.any = fabsf(bt.ny);
@@ -815,8 +839,10 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             bt.ang = -(float)rang[0];
             bt.aang = fabsf(bt.ang);
             bt.k = 8;  // the SurfaceArea partial sum adds eight overlaps
-            const int d = bound_decide(rm, n, c, rm.r, cl_total, bt, u_acc, cur, *star_iv,
-                                       a.bound_slack);
+            d = bound_decide(rm, n, c, rm.r, cl_total, bt, u_acc, cur, *star_iv, a.bound_slack);
+#if MH_DOUBLE & 256
+            }
+#endif
             if (r == 0) MH_PHASE(ch, 4, t0);
 #if MH_STAMPS
             if (r == 0) {
@@ -1343,7 +1369,13 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         s.pad = a.clrc[i].src;
         clrs_l[i] = s;
     }
-    for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) relc_l[i] = a.relc[i];
+    uint2* rix_l = reinterpret_cast<uint2*>(lds + a.lay.h_rix);
+    for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) {
+        const RelConst rc = a.relc[i];
+        relc_l[i] = rc;
+        rix_l[i] = make_uint2((unsigned)rc.s | ((unsigned)rc.t << 16),
+                              (unsigned)rc.as | ((unsigned)rc.at << 16));
+    }
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + F.h_room);
     if (threadIdx.x == 0) *rm_l = a.rm;
@@ -1362,6 +1394,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.objs = objs_l;
     ch.clrs = clrs_l;
     ch.relc = relc_l;
+    ch.rix = rix_l;
     ch.P = reinterpret_cast<ObjP*>(base + F.P);
     ch.PX = reinterpret_cast<double*>(base + F.PX);
     ch.PY = reinterpret_cast<double*>(base + F.PY);

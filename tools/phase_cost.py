@@ -10,7 +10,8 @@ from collections import defaultdict
 NAMES = {"2": "ablate per-object atan2/cos", "16": "ablate PW/ANG terms", "dbl1": "A per-object",
          "dbl2": "B full symmetry", "dbl64": "B delta symmetry",
          "dbl4": "E surface area walk", "dbl8": "E clearance",
-         "dbl16": "F pairwise appends", "dbl32": "G replay"}
+         "dbl16": "F pairwise appends", "dbl32": "G replay",
+         "dbl128": "C clearance pair update", "dbl256": "D bound terms + sums"}
 
 
 def load(d, kernel):
@@ -34,9 +35,10 @@ def main():
     a = ap.parse_args()
     steps = a.chains * a.iters
     base = load(os.path.join(a.tag_dir, "pmc_0"), a.kernel)
-    keys = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
+    keys = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
             "SQ_ACTIVE_INST_VALU", "ns"]
-    hdr = f"{'phase':28s}" + "".join(f"{k.replace('SQ_INSTS_', '').replace('SQ_ACTIVE_INST_', 'act_'):>11s}" for k in keys)
+    keys = [k for k in keys if k in base]
+    hdr = f"{'phase':28s}" + "".join(f"{k.replace('SQ_INSTS_', '').replace('SQ_ACTIVE_INST_', 'act_').replace('SQ_LDS_BANK_CONFLICT', 'ldsconf'):>11s}" for k in keys)
     print(hdr)
     print(f"{'whole step':28s}" + "".join(f"{base[k] / (steps if k != 'ns' else 1):11.1f}" for k in keys))
     # probe builds (dblK: phase run twice, +cost) and ablations (K: phase compiled out, -cost)
