@@ -134,7 +134,9 @@ def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str):
         return {}
     try:
         d = json.loads(p.read_text())
-        kind = "incremental" if "delta" in d.get("kernel", "") else "full"
+        k = d.get("kernel", "")
+        kind = ("incremental" if "delta" in k else
+                "full-few" if "mh_kernel<64, 1, 6>" in k else "full")
         if int(d.get("chains_per_launch", -1)) != n_chains_per_launch or kind != step_kernel:
             return {}
         return d

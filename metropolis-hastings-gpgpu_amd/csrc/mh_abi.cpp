@@ -217,6 +217,7 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
 
 struct Geometry {
     int L, npl, waves;   // full-evaluation kernel (init, final, evaluation; step when !delta)
+    bool few;            // step with OP_STEP_FEW (no register cap: too few chains to use it)
     mh::ChainLds lay;    // init / step
     int waves_ol;
     mh::ChainLds lay_ol; // final / evaluation (with the OffLimits boxes)
@@ -290,6 +291,12 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, Geometry
         const int w = atoi(e);
         if (w >= 1 && w <= 8 && mh::lds_bytes(g.lay, g.L, w) <= (size_t)max_lds) g.waves = w;
     }
+    // At most two chains per SIMD: the step kernel's register cap (five resident waves per SIMD)
+    // buys nothing, and its spills lengthen every step (config 2: 1.92e8 chain-steps/s uncapped
+    // against 1.77e8). $MH_STEP_FEW=0/1 forces the choice.
+    g.few = g.L == 64 && g.npl <= 1 && n_chains <= 8LL * cus;
+    if (const char* e = getenv("MH_STEP_FEW"))
+        if (*e) g.few = g.L == 64 && g.npl <= 1 && atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
     g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
@@ -512,7 +519,8 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
             chunk = (int)std::min<int64_t>(chunk, s->swap_interval - s->steps_done % s->swap_interval);
         a.iterations = chunk;
         if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dwaves, st));
-        else MH_TRY_HIP(mh::launch(mh::OP_STEP, a, s->geo.L, s->geo.npl, s->geo.waves, st));
+        else MH_TRY_HIP(mh::launch(s->geo.few ? mh::OP_STEP_FEW : mh::OP_STEP, a, s->geo.L,
+                                   s->geo.npl, s->geo.waves, st));
         done += chunk;
         s->steps_done += chunk;
         if (s->n_temps > 1 && s->steps_done % s->swap_interval == 0)
@@ -895,7 +903,7 @@ MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* c
     const int w = s->geo.delta ? s->geo.dwaves : s->geo.waves;
     if (lanes_per_chain) *lanes_per_chain = L;
     if (chains_per_workgroup) *chains_per_workgroup = w * (64 / L);
-    if (incremental) *incremental = s->geo.delta ? 1 : 0;
+    if (incremental) *incremental = s->geo.delta ? 1 : (s->geo.few ? 2 : 0);
     return 0;
 }
 
@@ -909,7 +917,7 @@ MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
         *chains_per_cu = blocks * g.dwaves;
     } else {
         blocks = mh::step_blocks_per_cu(g.L, g.npl, g.waves,
-                                        mh::lds_bytes(s->geo.lay, g.L, g.waves));
+                                        mh::lds_bytes(s->geo.lay, g.L, g.waves), g.few);
         *chains_per_cu = blocks * g.waves * (64 / g.L);
     }
     return 0;

@@ -1315,7 +1315,11 @@ __device__ __forceinline__ void restore(const ChainPtrs& ch, OwnPose<NPL>& op, i
 // Waves per SIMD the register allocator must leave room for. The plain step kernel with one
 // chain per wavefront and one object per lane (config 3) is held to 5: its LDS then admits five
 // 4-wave workgroups per CU, and 20 resident chains measured 4.47e8 chain-steps/s against 4.20e8
-// with 16 (101 VGPRs). Other instances keep the allocator's choice. $MH_WAVES_PER_EU builds
+// with 16 (101 VGPRs). Other instances keep the allocator's choice, among them OP_STEP_FEW, the
+// same step for launches of at most two chains per SIMD: at config 2 (N = 8, 1,024 chains, one
+// wavefront per SIMD) the cap's spills and reloads sit on the critical path, and the uncapped
+// build (122 VGPRs, no scratch) ran 1.92e8 chain-steps/s against 1.77e8 (gpurun_out/ab8a).
+// $MH_WAVES_PER_EU builds
 // (tools/build_ablate.sh wpeK) pin every instance for experiments.
 template <int L, int NPL, int OP>
 struct StepWaves {
@@ -1339,7 +1343,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // OP_STEP_T: OP_STEP with best-of-chain tracking compiled in; OP_STEP_XW: the same drawing
     // from the cuRAND XORWOW stream instead of Philox. Plain OP_STEP carries no tracking code.
-    constexpr bool STEP = (OP == OP_STEP || OP == OP_STEP_T || OP == OP_STEP_XW);
+    constexpr bool STEP =
+        (OP == OP_STEP || OP == OP_STEP_T || OP == OP_STEP_XW || OP == OP_STEP_FEW);
     constexpr bool TRACK = (OP == OP_STEP_T || OP == OP_STEP_XW);
     // (one chain per wave draws from the wave-batched Philox window, its Box-Muller pairs in LDS)
     using Rng = typename std::conditional<OP != OP_STEP_XW && L == 64, WaveRngLds,
@@ -1955,6 +1960,12 @@ static hipError_t launch_geom(int op, const LaunchArgs& a, int waves_per_wg, hip
     switch (op) {
         case OP_INIT: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_INIT>), grid, block, lds, stream, a); break;
         case OP_STEP: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_STEP>), grid, block, lds, stream, a); break;
+        case OP_STEP_FEW:
+            if constexpr (L == 64 && NPL == 1)
+                hipLaunchKernelGGL((mh_kernel<64, 1, OP_STEP_FEW>), grid, block, lds, stream, a);
+            else
+                hipLaunchKernelGGL((mh_kernel<L, NPL, OP_STEP>), grid, block, lds, stream, a);
+            break;
         case OP_FINAL: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_FINAL>), grid, block, lds, stream, a); break;
         default: hipLaunchKernelGGL((mh_kernel<L, NPL, OP_EVAL>), grid, block, lds, stream, a); break;
     }
@@ -1989,23 +2000,25 @@ int max_npl() { return 8; }
 // Resident workgroups per CU of the plain step kernel for a launch shape (registers, LDS and
 // the wave limit, as the runtime counts them). 0 if it does not fit.
 template <int L>
-static int step_blocks_l(int npl, int threads, size_t lds) {
+static int step_blocks_l(int npl, int threads, size_t lds, bool few) {
     int blocks = 0;
     hipError_t e;
-    if (npl <= 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 1, OP_STEP>, threads, lds);
+    if (few && L == 64 && npl <= 1)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<64, 1, OP_STEP_FEW>, threads, lds);
+    else if (npl <= 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 1, OP_STEP>, threads, lds);
     else if (npl <= 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 2, OP_STEP>, threads, lds);
     else if (npl <= 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 4, OP_STEP>, threads, lds);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_kernel<L, 8, OP_STEP>, threads, lds);
     return e == hipSuccess ? blocks : 0;
 }
 
-int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds) {
+int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds, bool few) {
     const int threads = 64 * waves_per_wg;
     switch (L) {
-        case 8: return step_blocks_l<8>(npl, threads, lds);
-        case 16: return step_blocks_l<16>(npl, threads, lds);
-        case 32: return step_blocks_l<32>(npl, threads, lds);
-        default: return step_blocks_l<64>(npl, threads, lds);
+        case 8: return step_blocks_l<8>(npl, threads, lds, false);
+        case 16: return step_blocks_l<16>(npl, threads, lds, false);
+        case 32: return step_blocks_l<32>(npl, threads, lds, false);
+        default: return step_blocks_l<64>(npl, threads, lds, few);
     }
 }
 
@@ -2015,8 +2028,9 @@ size_t lds_bytes(const ChainLds& lay, int L, int waves_per_wg) {
 
 hipError_t launch(int op, const LaunchArgs& a, int L, int npl, int waves_per_wg, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
-    if (op == OP_STEP && a.rng == RNG_CURAND_XORWOW) return launch_step_xw(a, L, npl, waves_per_wg, s);
-    if (op == OP_STEP && (a.track != TRACK_OFF || a.n_temps > 1))
+    const bool step = op == OP_STEP || op == OP_STEP_FEW;
+    if (step && a.rng == RNG_CURAND_XORWOW) return launch_step_xw(a, L, npl, waves_per_wg, s);
+    if (step && (a.track != TRACK_OFF || a.n_temps > 1))
         return launch_step_best(a, L, npl, waves_per_wg, s);
     // (lanes per chain, objects per lane) instantiations; npl rounds up to the next one.
     switch (L) {

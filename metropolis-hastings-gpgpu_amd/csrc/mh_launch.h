@@ -11,7 +11,11 @@
 
 namespace mh {
 
-enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3, OP_STEP_XW = 4, OP_STEP_T = 5 };
+// OP_STEP_FEW: OP_STEP compiled without the step kernel's register cap, for launches with too few
+// chains to use the resident waves the cap buys (mh_abi.cpp choose_geometry; one chain per
+// wavefront, one object per lane only).
+enum Op { OP_INIT = 0, OP_STEP = 1, OP_FINAL = 2, OP_EVAL = 3, OP_STEP_XW = 4, OP_STEP_T = 5,
+          OP_STEP_FEW = 6 };
 
 // Which stream the chains draw from (mh_options.rng).
 enum RngKind { RNG_PHILOX = 0, RNG_CURAND_XORWOW = 1 };
@@ -51,7 +55,7 @@ size_t delta_lds_bytes(const DeltaLds& lay, int waves_per_wg);
 hipError_t launch_delta(const LaunchArgs& a, int waves_per_wg, hipStream_t s);
 int delta_blocks_per_cu(int n, int waves_per_wg, size_t lds_bytes);
 int delta_max_waves(int n);  // chains per workgroup the incremental kernel admits
-int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds_bytes);
+int step_blocks_per_cu(int L, int npl, int waves_per_wg, size_t lds_bytes, bool few);
 hipError_t launch_summary(const resultCosts* costs, const ChainMeta* meta, int64_t n,
                           int64_t chain_offset, mh_summary* out, hipStream_t s);
 hipError_t launch_collectives(int L, const float* v, const int* iv, int* out, hipStream_t s);

@@ -321,7 +321,7 @@ def test_incremental_list_overflow_windows(mh, orc, hiplib, monkeypatch, waves):
     assert c * n > 4 * np_pad  # the list cannot fit: windows on every step
     chains, steps, seed = 16, 120, 160
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == "incremental" and s.step_kernel()[0] == 64
+        assert s.step_kernel()[2].split("-")[0] == "incremental" and s.step_kernel()[0] == 64
         if waves:
             assert s.step_kernel()[1] == int(waves)
         s.run(steps)

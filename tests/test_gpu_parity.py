@@ -43,18 +43,24 @@ def _narrow_lanes(n: int) -> int:
     return L
 
 
-STEPS = ["incremental", "full", "full-narrow"]
+STEPS = ["incremental", "full", "full-narrow", "full-capped"]
 
 
 def _use_step(monkeypatch, step: str, n: int) -> str:
     """Selects the step kernel (MH_DELTA) and, for "full-narrow", the narrow width (MH_LANES);
-    returns the step-kernel kind the session must report."""
+    "full-capped" forces the register-capped instance of the one-chain-per-wavefront step that
+    launches of many chains use (these tests' few chains get the uncapped OP_STEP_FEW one).
+    Returns the step-kernel kind the session must report."""
     kind = step.split("-")[0]
     monkeypatch.setenv("MH_DELTA", "1" if kind == "incremental" else "0")
     if step == "full-narrow":
         if _narrow_lanes(n) == 64:
             pytest.skip("the narrow instance is the default one for this N")
         monkeypatch.setenv("MH_LANES", str(_narrow_lanes(n)))
+    if step == "full-capped":
+        if n > 64:
+            pytest.skip("one object per lane only")
+        monkeypatch.setenv("MH_STEP_FEW", "0")
     return kind
 
 
@@ -181,7 +187,9 @@ def test_chains_match_oracle_each_step_kernel(mh, orc, hiplib, monkeypatch, step
     room = _room(mh, kind, n)
     seed = 7000 + n
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == kind_
+        assert s.step_kernel()[2].split("-")[0] == kind_
+        if step in ("full", "full-capped") and n <= 64:  # (which one-object-per-lane instance)
+            assert s.step_kernel()[2] == ("full-few" if step == "full" else "full")
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -276,7 +284,7 @@ def test_running_costs_equal_fresh_evaluation(mh, hiplib, monkeypatch, step, n, 
     monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
     room = mh.synthetic_room(n)
     with mh.Session(room, chains, seed=77 + n) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2].split("-")[0] == step
         s.run(steps)
         s.finalize()
         _, fresh = s.download()
@@ -365,7 +373,7 @@ def test_best_of_chain_matches_oracle(mh, orc, hiplib, monkeypatch, step, track,
     room = _room(mh, kind, n)
     seed = 9100 + n + track
     with mh.Session(room, chains, seed=seed, track=track) as s:
-        assert s.step_kernel()[2] == kind_
+        assert s.step_kernel()[2].split("-")[0] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -470,7 +478,7 @@ def test_xorwow_chains_match_oracle(mh, orc, hiplib, monkeypatch, step, kind, n,
     room = _room(mh, kind, n)
     seed = 1760000000 + n
     with mh.Session(room, chains, seed=seed, rng=1) as s:
-        assert s.step_kernel()[2] == kind_
+        assert s.step_kernel()[2].split("-")[0] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -510,7 +518,7 @@ def test_maximum_room_size(mh, orc, hiplib, monkeypatch, step, n):
     room = mh.synthetic_room(n)
     chains, steps, seed = 8, 30, 512
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2].split("-")[0] == step
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -543,7 +551,7 @@ def test_tempering_matches_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, K
     room = _room(mh, kind, n)
     seed = 3100 + n + K
     with mh.Session(room, chains, seed=seed, temps=K, swap_interval=interval, beta_min=0.2) as s:
-        assert s.step_kernel()[2] == kind_
+        assert s.step_kernel()[2].split("-")[0] == kind_
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -599,7 +607,7 @@ def test_wave_rng_window_overrun(mh, orc, hiplib, monkeypatch, step):
         room.cfg[i].frozen = True
     chains, steps, seed = 64, 1300, 606
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[:1] == (64,) and s.step_kernel()[2] == step
+        assert s.step_kernel()[:1] == (64,) and s.step_kernel()[2].split("-")[0] == step
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -622,7 +630,7 @@ def test_stacked_objects_symmetry_ties(mh, orc, hiplib, monkeypatch, step, n, ch
         room.cfg[i].frozen = i % 2 == 1
     seed = 8800 + n
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == step
+        assert s.step_kernel()[2].split("-")[0] == step
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -651,7 +659,7 @@ def test_bound_decision_paths(mh, orc, hiplib, monkeypatch, step, slack, kind, n
     room = _room(mh, kind, n)
     seed = 9100 + n
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel()[2] == kind_
+        assert s.step_kernel()[2].split("-")[0] == kind_
         s.run(steps)
         cur = s.current_costs()
         s.finalize()
