@@ -349,7 +349,7 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
 #define MH_EVAL_ATTR __attribute__((noinline))
 #endif
 
-template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false>
+template <int L, int NPL, bool WITH_OL, bool DELTA, bool FAST = false, bool PAIRS = false>
 __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch, const OwnPose<NPL>& op,
                            int r, int gbase,
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
@@ -577,11 +577,43 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         }
     }
     } else {
+    // PAIRS (the few-chains instance) with at most 8 objects: all N^2 pairs at once, lane
+    // 8 i + j evaluating pair (i, j) exactly as the reference does, then each 8-lane group's
+    // maximum (floored at 0, Kernel.cu:303-311; max is exact, so the order does not matter) and
+    // its lowest column go to row i's owner lane. One exact evaluation on the step's critical
+    // path instead of the screened passes below, which a wavefront per SIMD waits out in full.
+    bool pairs_done = false;
+    if constexpr (PAIRS && L == 64 && NPL == 1) {
+        if (n <= 8) {
+            const int pi = r >> 3, pj = r & 7;
+            const int ai = pi << 2, aj = pj << 2;
+            const float prx = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rxs[0])));
+            const float pry = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rys[0])));
+            const float prr = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rrs[0])));
+            const int2 w = *reinterpret_cast<const int2*>(&op.ry[0]);
+            int2 o;
+            o.x = __builtin_amdgcn_ds_bpermute(aj, w.x);
+            o.y = __builtin_amdgcn_ds_bpermute(aj, w.y);
+            const double ryj = *reinterpret_cast<const double*>(&o);
+            const ObjP q = ch.P[pj];
+            float v = 0.0f;
+            if (pi < n && pj < n)
+                v = fmaxf(0.0f, sym_val_exact(q.xf, q.yf, ryj, prx, pry, (double)prr));
+            int j = v > 0.0f ? pj : 8;
+            group_max_arg<8>(v, j);
+            const int src = (r & 7) << 5;  // lane 8 r holds row r's maximum
+            const float mx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v)));
+            const int ag = __builtin_amdgcn_ds_bpermute(src, j);
+            sym.mx[0] = r < n ? mx : 0.0f;
+            sym.arg[0] = (r < n && ag < 8) ? ag : -1;
+            pairs_done = true;
+        }
+    }
     // Delta: only rows ka, kb and columns ka, kb changed. An unchanged row keeps its maximum
     // unless a changed column beats it (screened by the estimate) or its argmax column is a
     // changed one whose value dropped; changed rows and such rows are re-scanned by the whole
     // group, one row at a time.
-    for (int rep = 0; rep < MH_REPS(64); ++rep) {
+    for (int rep = 0; rep < MH_REPS(64) && !pairs_done; ++rep) {
     MH_CLOBBER();
     bool need[NPL];
     unsigned pend[NPL];
@@ -1521,8 +1553,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             CostIv star_iv{0.0f, 0.0f};
             float u_acc = 0.0f;
             if constexpr (FASTK) u_acc = rng.uniform();
-            eval_costs<L, NPL, false, true, FASTK>(a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y,
-                                                    cls, cl, u_acc, cur_iv, &fast, &star_iv);
+            eval_costs<L, NPL, false, true, FASTK, OP == OP_STEP_FEW>(
+                a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y, cls, cl, u_acc, cur_iv, &fast,
+                &star_iv);
             MH_STAMP(ts);
 #if MH_CHECK
             if constexpr (FASTK)
