@@ -123,7 +123,17 @@ struct ChainPtrs {
     ChainAux* aux;
     const DevRoom* rm;  // LDS copy of the room scalars
     const double* zero4;  // four zero doubles (a finished replay lane reads these)
+    // (few-chains instance) lane r's own room records, held in registers for the launch: object
+    // r's and clearance r's shapes, relationship r and its packed objects
+    RectShape lo, lc;
+    RelConst lr;
+    uint2 lx;
 };
+
+// Whether a kernel instance holds the lane's room records in registers (ChainPtrs::lo ...).
+#ifndef MH_HOIST_FEW
+#define MH_HOIST_FEW ((MH_OPT & 64) != 0)
+#endif
 
 // ---- compacted term lists for the ordered sums -------------------------------------------
 //
@@ -196,6 +206,7 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
 // atan2, double cos rounded to float, double distance and divisions, Kernel.cu:170-188,
 // 210-281); one shared atan2 pass serves a lane's relationship or, failing that, its object, and
 // a lane that needs both takes a second (rare) pass.
+template <bool HOIST = false>
 __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
                                             bool obj, bool rel, float& cph, double& rpw,
                                             double& rang) {
@@ -203,7 +214,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
     double dy = fy, dx = fx, tpw = 0.0;
     float ti = 0.0f;
-    if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
+    if (rel) tpw = rel_pair(HOIST ? ch.lr : ch.relc[i], ch.P, dy, dx, ti);
     double a1 = 0.0, a2 = 0.0;
     if (rel || obj) a1 = atan2(dy, dx);
     if (rel && obj) a2 = atan2(fy, fx);
@@ -215,7 +226,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     }
     if (rel) {
         rpw = tpw;
-        rang = rel_angle(ch.relc[i], a1, ti);
+        rang = rel_angle(HOIST ? ch.lr : ch.relc[i], a1, ti);
     }
 }
 
@@ -224,6 +235,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
 // estimate lies too near one of the reference's discontinuities for its branch to be certain --
 // the distance range's ends (:216-221), theta's two wraps (:176-181), the wrapped range's fmodf
 // and switch (:245-250) -- or the range normaliser is degenerate; such a lane needs exact_terms().
+template <bool HOIST = false>
 __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
                                              bool obj, bool rel, float& cph, double& rpw,
                                              double& rang, float& eang, bool& amb) {
@@ -235,7 +247,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
         cph = cosf(b + (float)kHalfPI);
     }
     if (rel) {
-        const RelConst& rc = ch.relc[i];
+        const RelConst& rc = HOIST ? ch.lr : ch.relc[i];
         const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
         const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;  // (the reference's float differences)
         const float d = __builtin_sqrtf(fx * fx + fy * fy);   // within 2 U of its double distance
@@ -279,7 +291,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
 // carry; the others keep their zero / non-zero state. Updates this lane's column mask and the
 // proposed row words (the other LDS buffer), writes the row prefix counts of the proposed rows
 // and returns the number of non-zero pairs (Kernel.cu:408-431 terms that are not exactly zero).
-template <int L>
+template <int L, bool HOIST = false>
 __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, int ka, int kb,
                                              int r, int gbase, float4 boxj, const ClPairs& clp,
                                              ClPairs& clo, bool& colchg) {
@@ -301,8 +313,8 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
         w = (w & ~(1ull << k)) | ((uint64_t)nzk << k);
     }
     // rows of the clearances whose source moved: every object lane re-tests its pair
-    uint64_t moved = group_ballot<L>(r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb),
-                                     gbase);
+    const int src = r < c ? (HOIST ? ch.lc.pad : ch.clrs[r].pad) : -2;
+    uint64_t moved = group_ballot<L>(src == ka || src == kb, gbase);
     while (moved) {
         const int i = __builtin_ctzll(moved);
         moved &= moved - 1;
@@ -358,8 +370,11 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                            CostIv* star_iv = nullptr) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
-    const DevRoom& rm = *ch.rm;
+    // (the few-chains instance reads them from the kernel arguments: no LDS round trip on its
+    // latency-bound step; config 2 4.30 -> 4.25 ms per 1,000-step launch)
+    const DevRoom& rm = PAIRS ? a.rm : *ch.rm;
     const int n = a.rm.n, c = a.rm.c;
+    constexpr bool HOIST = PAIRS && MH_HOIST_FEW;  // (lane r's room records in registers)
 
     unsigned long long t0 = 0;
     MH_STAMP(t0);
@@ -391,7 +406,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const bool moved = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
             bool touched = false;
             if (i < rm.r && !(MH_ABLATE & 16)) {
-                const uint2 q = ch.rix[i];
+                const uint2 q = HOIST ? ch.lx : ch.rix[i];
                 const unsigned a16 = (unsigned)ka, b16 = (unsigned)kb;  // (ka, kb < 65536)
                 touched = ka >= 0 && ((q.x & 0xffffu) == a16 || (q.x >> 16) == a16 ||
                                       (q.y & 0xffffu) == a16 || (q.y >> 16) == a16 ||
@@ -407,7 +422,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             if constexpr (FAST) {
                 bool amb = false;
                 if (__ballot(moved || touched))
-                    approx_terms(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
+                    approx_terms<HOIST>(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
                                  amb);
                 clo.dc = clo.dc || moved;
                 clo.dr = clo.dr || touched;
@@ -416,20 +431,28 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                         clo.dr = false;
                         clo.eang = 0.0f;
                     }
-                    exact_terms(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
+                    exact_terms<HOIST>(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
                 }
             } else {
                 const bool obj = moved || (i < n && clp.dc);
                 const bool rel = touched || (i < rm.r && clp.dr);
-                if (__ballot(obj || rel)) exact_terms(ch, rm, i, n, obj, rel, cph[m], rpw[m], rang[m]);
+                if (__ballot(obj || rel))
+                    exact_terms<HOIST>(ch, rm, i, n, obj, rel, cph[m], rpw[m], rang[m]);
                 clo.dc = clo.dr = false;
                 clo.eang = 0.0f;
             }
         }
         if (i < n) {
-            const RectShape os = ch.objs[i];
+            const RectShape os = HOIST ? ch.lo : ch.objs[i];
             const float area = __int_as_float(os.pad);
-            const ObjP p = ch.P[i];
+            ObjP p;
+            if constexpr (HOIST) {  // (the float pose words are the registers' poses rounded)
+                p.xf = (float)op.x[m];
+                p.yf = (float)op.y[m];
+                p.rotYf = (float)op.ry[m];
+            } else {
+                p = ch.P[i];
+            }
             const double x = op.x[m], y = op.y[m];
             wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(op.ry[m]) < 1e15);
             // VisualBalanceCosts products, Kernel.cu:200-201.
@@ -471,7 +494,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             }
         }
         if (i < c) {
-            const RectShape cs = ch.clrs[i];
+            const RectShape cs = HOIST ? ch.lc : ch.clrs[i];
             const ObjP ps = ch.P[cs.pad];
             ch.CLA[i] = shape_box(cs, ps.xf, ps.yf);             // ClearanceCosts, :414-415
         }
@@ -483,8 +506,14 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             sa_new = sa_new && (i == ka || i == kb);
         }
         if (sa_new) {
-            const ObjP pi = ch.P[i];
-            sac[m] = comp_overlaps(rm, shape_box(ch.clrs[i], pi.xf, pi.yf));
+            ObjP pi;
+            if (HOIST && i < n) {  // (a clearance past the objects reads the pose words as before)
+                pi.xf = (float)op.x[m];
+                pi.yf = (float)op.y[m];
+            } else {
+                pi = ch.P[i];
+            }
+            sac[m] = comp_overlaps(rm, shape_box(HOIST ? ch.lc : ch.clrs[i], pi.xf, pi.yf));
         }
         if constexpr (NPL == 1) clo.sac = sac[0];
     }
@@ -499,6 +528,12 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // bound is proven for (exact_mode) evaluates every pair exactly.
     if (r == 0) MH_PHASE(ch, 1, t0);
     const bool exact_mode = group_ballot<L>(wild, gbase) != 0;
+    // Steps that decide on the rejection bound leave a re-scanned row's maximum as its leader's
+    // fp32 estimate (the bound adds its allowance, esym); the leader's exact value is evaluated
+    // only if the step is not certainly rejected (below), when the row enters a commit or a sum.
+    constexpr bool DEFER_SYM = FAST;  // (one chain per wavefront, one object per lane)
+    int dlead = -1;
+    float esym = 0.0f;
     if constexpr (!DELTA) {
     // Full scan: keep the two largest estimates per row and evaluate the leader exactly. When
     // the top two are closer than their error bounds the row falls back to the exact value of
@@ -752,7 +787,11 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         for (int m = 0; m < NPL; ++m) {
             if (m == ms) {
                 if (r == b) {
-                    if (clear) {
+                    if (clear && DEFER_SYM) {
+                        dlead = ld.j;
+                        esym = sym_err(ld.m, rr);
+                        sym.mx[m] = fmaxf(0.0f, ld.m);
+                    } else if (clear) {
                         lead[m] = ld.j;
                         leadp |= 1u << m;
                     } else {
@@ -803,7 +842,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             MH_CLOBBER();
             colchg = colchg0;
 #endif
-            cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo, colchg);
+            cl_total = inc_cl_update<L, HOIST>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo,
+                                               colchg);
 #if MH_DOUBLE & 128
         }
 #endif
@@ -857,7 +897,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             bt.fp = -cph[0];
             bt.afp = fabsf(bt.fp);
             bt.sym = -sym.mx[0];
-            bt.symw = r < n ? (float)(n - r) * sym.mx[0] : 0.0f;  // (row r: position r)
+            bt.symw = r < n ? (float)(n - r) * (sym.mx[0] + esym) : 0.0f;  // (row r: position r)
+            bt.esym = esym;
             bt.cl = -clsum;
             bt.kcl = kcl;
             bt.clpos = 0.0f;  // (no position credit: the list positions are not formed here)
@@ -883,16 +924,36 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                 ch.aux->cyc[10] += d == BOUND_ACCEPT ? 1 : 0;
             }
 #endif
-            if (d != BOUND_OPEN) {
+            if (d == BOUND_REJECT) {
                 *fast = d;
                 return;
+            }
+            if constexpr (DEFER_SYM) {
+                // the deferred leaders' exact values (every lane active for the rotY read)
+                if (__ballot(dlead >= 0)) {
+                    const int j = dlead >= 0 ? dlead : 0;
+                    const double ryj = pose_ry_var<L, NPL>(op, j, gbase);
+                    if (dlead >= 0) {
+                        const ObjP q = ch.P[j];
+                        const float e = sym_val_exact(q.xf, q.yf, ryj, rxs[0], rys[0],
+                                                      (double)rrs[0]);
+                        MH_CK(fabsf(fmaxf(0.0f, e) - sym.mx[0]) <= esym, 33,
+                              __float_as_uint(e), __float_as_uint(sym.mx[0]));
+                        sym.mx[0] = fmaxf(0.0f, e);
+                        sym.arg[0] = e > 0.0f ? j : -1;
+                    }
+                }
+                if (d != BOUND_OPEN) {
+                    *fast = d;
+                    return;
+                }
             }
             // The exact sums are needed: every estimated term is made exact first.
             const bool obj = r < n && clo.dc, rel = r < rm.r && clo.dr;
             if (__ballot(obj || rel)) {
                 float c0 = cph[0];
                 double p0 = rpw[0], a0 = rang[0];
-                exact_terms(ch, rm, r, n, obj, rel, c0, p0, a0);
+                exact_terms<HOIST>(ch, rm, r, n, obj, rel, c0, p0, a0);
 #if MH_CHECK
                 // the estimates' allowances, against the exact values
                 MH_CK(!obj || fabsf(cph[0] - c0) <= kDeltaCph, 30, __float_as_uint(cph[0]),
@@ -1449,6 +1510,12 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
     ch.zero4 = reinterpret_cast<const double*>(lds + F.h_zero);
+    if constexpr (OP == OP_STEP_FEW && MH_HOIST_FEW) {
+        ch.lo = objs_l[r < n ? r : 0];
+        ch.lc = clrs_l[r < a.rm.c ? r : 0];
+        ch.lr = relc_l[r < a.rm.r ? r : 0];
+        ch.lx = rix_l[r < a.rm.r ? r : 0];
+    }
 
     // Zero the dense replay streams past N (never written afterwards).
     for (int i = n + r; i < a.lay.N4; i += L) {
@@ -1536,7 +1603,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             unsigned long long ts = 0;
             MH_STAMP(ts);
             rng_prepare(rng);
-            const int2 kk = propose<L, NPL>(rng, *rm_l, frozen, ch, op, r, gbase, writer);
+            const int2 kk = propose<L, NPL>(rng, OP == OP_STEP_FEW ? a.rm : *rm_l, frozen, ch, op,
+                                            r, gbase, writer);
             MH_CK(kk.x < n && kk.y < n && kk.x >= -1 && kk.y >= -1, 11, kk.x, kk.y);
             wave_sync();
             if (writer) MH_PHASE(ch, 0, ts);

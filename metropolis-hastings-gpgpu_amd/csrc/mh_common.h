@@ -16,6 +16,10 @@
 #define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
 #endif
 
+#ifndef MH_OPT
+#define MH_OPT 0  // A/B switches of optimisations under measurement (bit per change)
+#endif
+
 #ifndef MH_CHECK
 #define MH_CHECK 0  // debug builds: computed global / LDS indices validated and every decision of
                     // the rejection bound verified against the exact costs, the first violation
@@ -750,6 +754,8 @@ struct BoundTerms {
                              // (bound_decide<true>: the two sums in fp64)
     float efp;               // absolute error of this lane's FocalPoint terms (fp32 estimates)
     float eang;              // absolute error of this lane's PairWiseAngle terms (estimates)
+    float esym;              // absolute error of this lane's Symmetry row maximum (an fp32
+                             // estimate whose exact value the step has not needed yet)
     int pwx;                 // relative error of estimated PairWise terms, in U (uniform)
     int k;                   // most terms any lane pre-sums into any other partial sum (the
                              // same value on every lane: it enters the uniform bound)
@@ -886,7 +892,7 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const float elin = (26.0f + kf + eacc) * U * afp + (26.0f + kf) * U * fabsf(lsym) +
                        U * wsym + (26.0f + (float)bt.kcl) * U * fabsf(lcl) + U * wcl +
                        (4.0f * (c + n) + 26.0f + kf) * U * fabsf(lsa) + 12.0f * U * alin +
-                       fabsf(rm.w_fp) * bt.efp;
+                       fabsf(rm.w_fp) * bt.efp + fabsf(rm.w_sym) * bt.esym;
     // (fp32 path: the PairWise sum's relative allowance, estimates included; the angle terms'
     // absolute allowances enter its magnitude sum scaled by 1 / cr, so eang = cr a_ang covers them)
     const float cr32 = (26.0f + kf + eacc + (float)bt.pwx) * U;
@@ -1090,6 +1096,7 @@ __device__ __forceinline__ int pick_object(Rng& rng, int n, const unsigned char*
     while (frozen[k]) k = rand_int(rng, n - 1, 0);  // frozen[n] == 1: index n is redrawn
     return k;
 }
+
 
 // Accept(), Kernel.cu:706-713 (maximisation, BETA = 2).
 // The threshold min(1, (float)exp(x)) of Accept without evaluating exp where it is decided:

@@ -580,7 +580,7 @@ __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, con
     bt.symw = bt.clpos = 0.0f;
     bt.pw = bt.ang = bt.aang = 0.0f;
     bt.pwd = bt.angd = 0.0;
-    bt.efp = bt.eang = 0.0f;  // (exact terms only)
+    bt.efp = bt.eang = bt.esym = 0.0f;  // (exact terms only)
     bt.pwx = 0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {

@@ -12,7 +12,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-LIB = ROOT / "metropolis-hastings-gpgpu_amd" / "libmhgpu_check.so"  # (__graft_entry__.build())
+LIB = Path(os.environ.get("MH_CHECK_LIB", ROOT / "metropolis-hastings-gpgpu_amd" /
+                         "libmhgpu_check.so"))  # (__graft_entry__.build())
 SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept rejects",
          22: "exact total outside the bound's interval",
          23: "current total outside the carried interval",
@@ -21,7 +22,8 @@ SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept
          26: "a launch ended without the current configuration's exact costs",
          27: "cached Clearance row sums differ from a fresh build",
          28: "cached Clearance column sum differs from a fresh one",
-         29: "cached SurfaceArea sums differ from a fresh build"}
+         29: "cached SurfaceArea sums differ from a fresh build",
+         33: "a deferred Symmetry row maximum outside its estimate's allowance"}
 
 # (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
 # object far outside the proven symmetry range, "negw" flips the weights' signs.
