@@ -123,17 +123,7 @@ struct ChainPtrs {
     ChainAux* aux;
     const DevRoom* rm;  // LDS copy of the room scalars
     const double* zero4;  // four zero doubles (a finished replay lane reads these)
-    // (few-chains instance) lane r's own room records, held in registers for the launch: object
-    // r's and clearance r's shapes, relationship r and its packed objects
-    RectShape lo, lc;
-    RelConst lr;
-    uint2 lx;
 };
-
-// Whether a kernel instance holds the lane's room records in registers (ChainPtrs::lo ...).
-#ifndef MH_HOIST_FEW
-#define MH_HOIST_FEW ((MH_OPT & 64) != 0)
-#endif
 
 // ---- compacted term lists for the ordered sums -------------------------------------------
 //
@@ -206,7 +196,6 @@ __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tp
 // atan2, double cos rounded to float, double distance and divisions, Kernel.cu:170-188,
 // 210-281); one shared atan2 pass serves a lane's relationship or, failing that, its object, and
 // a lane that needs both takes a second (rare) pass.
-template <bool HOIST = false>
 __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
                                             bool obj, bool rel, float& cph, double& rpw,
                                             double& rang) {
@@ -214,7 +203,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
     double dy = fy, dx = fx, tpw = 0.0;
     float ti = 0.0f;
-    if (rel) tpw = rel_pair(HOIST ? ch.lr : ch.relc[i], ch.P, dy, dx, ti);
+    if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
     double a1 = 0.0, a2 = 0.0;
     if (rel || obj) a1 = atan2(dy, dx);
     if (rel && obj) a2 = atan2(fy, fx);
@@ -226,8 +215,50 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     }
     if (rel) {
         rpw = tpw;
-        rang = rel_angle(HOIST ? ch.lr : ch.relc[i], a1, ti);
+        rang = rel_angle(ch.relc[i], a1, ti);
     }
+}
+
+// The fp32 PairWise estimate of a relationship from its objects' pose words (the reference's float
+// differences; the distance within 2 U of its double value), setting `amb` near the range's ends.
+__device__ __forceinline__ double rel_pw_est(const RelConst& rc, ObjP ps, ObjP pt, bool& amb) {
+    constexpr float U = 0x1p-24f;
+    const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;
+    const float d = __builtin_sqrtf(fx * fx + fy * fy);
+    const float st = (float)rc.start, en = (float)rc.end;
+    amb |= fabsf(d - st) <= 8.0f * U * fabsf(st) || fabsf(d - en) <= 8.0f * U * fabsf(en);
+    float f = 0.0f;
+    if (d < st) f = d / st;
+    else if (d > en) f = en / d;
+    return (double)(f * f);
+}
+
+// The fp32 PairWiseAngle estimate from theta's atan2f `tp` of (dya, dxa) and the target's pose
+// words, with its absolute allowance `eang`; `amb` near theta's wraps and the range's switch.
+__device__ __forceinline__ double rel_ang_est(const RelConst& rc, ObjP atp, float tp, float dxa,
+                                              float dya, float& eang, bool& amb) {
+    constexpr float U = 0x1p-24f;
+    amb |= fabsf(tp) <= kDeltaTh && !(dxa == 0.0f && dya == 0.0f);
+    if (tp < 0.0f) tp = tp + (float)kTwoPI;
+    const float t = tp - atp.rotYf;
+    amb |= fabsf(t) <= kDeltaTh;
+    const float th = t < 0.0f ? t + (float)kTwoPI : t;
+    bool on;
+    double norm;
+    if (rc.amin > rc.amax) {
+        const float w = fmodf((float)(rc.amin + (double)th), (float)kTwoPI);
+        amb |= fabsf(w - (float)rc.amax) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
+               fabsf(w - (float)kTwoPI) <= 2.0f * kDeltaTh;
+        on = (double)w > rc.amax;
+        norm = rc.norm_w;
+    } else {
+        on = rc.amin < (double)th || (double)th < rc.amax;  // (continuous at its switch)
+        norm = rc.norm_n;
+    }
+    amb |= !(fabs(norm) >= 1e-3);
+    const double v = on ? fmin(fabs((double)th - rc.amin), fabs((double)th - rc.amax)) / norm : 0.0;
+    eang = (float)((double)(2.0f * kDeltaTh) / fabs(norm)) + 4.0f * U * (float)fabs(v);
+    return v;
 }
 
 // fp32 estimates of the same terms for the rejection bound (no double transcendental): cph
@@ -235,54 +266,51 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
 // estimate lies too near one of the reference's discontinuities for its branch to be certain --
 // the distance range's ends (:216-221), theta's two wraps (:176-181), the wrapped range's fmodf
 // and switch (:245-250) -- or the range normaliser is degenerate; such a lane needs exact_terms().
-template <bool HOIST = false>
+template <bool SHARE>
 __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
                                              bool obj, bool rel, float& cph, double& rpw,
                                              double& rang, float& eang, bool& amb) {
-    constexpr float U = 0x1p-24f;
-    if (obj) {
-        const ObjP p = ch.P[i < n ? i : 0];
-        const float at = atan2f(rm.fyf - p.yf, rm.fxf - p.xf);
-        const float b = at - p.rotYf;
-        cph = cosf(b + (float)kHalfPI);
-    }
-    if (rel) {
-        const RelConst& rc = HOIST ? ch.lr : ch.relc[i];
-        const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
-        const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;  // (the reference's float differences)
-        const float d = __builtin_sqrtf(fx * fx + fy * fy);   // within 2 U of its double distance
-        const float st = (float)rc.start, en = (float)rc.end;
-        amb |= fabsf(d - st) <= 8.0f * U * fabsf(st) || fabsf(d - en) <= 8.0f * U * fabsf(en);
-        float f = 0.0f;
-        if (d < st) f = d / st;
-        else if (d > en) f = en / d;
-        rpw = (double)(f * f);
-        const ObjP as = ch.P[rc.as], atp = ch.P[rc.at];
-        const float dxa = as.xf - atp.xf, dya = as.yf - atp.yf;
-        float tp = atan2f(dya, dxa);
-        amb |= fabsf(tp) <= kDeltaTh && !(dxa == 0.0f && dya == 0.0f);
-        if (tp < 0.0f) tp = tp + (float)kTwoPI;
-        const float t = tp - atp.rotYf;
-        amb |= fabsf(t) <= kDeltaTh;
-        const float th = t < 0.0f ? t + (float)kTwoPI : t;
-        bool on;
-        double norm;
-        if (rc.amin > rc.amax) {
-            const float w = fmodf((float)(rc.amin + (double)th), (float)kTwoPI);
-            amb |= fabsf(w - (float)rc.amax) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
-                   fabsf(w - (float)kTwoPI) <= 2.0f * kDeltaTh;
-            on = (double)w > rc.amax;
-            norm = rc.norm_w;
-        } else {
-            on = rc.amin < (double)th || (double)th < rc.amax;  // (continuous at its switch)
-            norm = rc.norm_n;
+    if constexpr (!SHARE) {
+        // (the latency-bound few-chains instance: two passes, the object's first -- 4.20
+        // against 4.24 ms per config-2 launch with the shared pass)
+        if (obj) {
+            const ObjP p = ch.P[i < n ? i : 0];
+            const float at = atan2f(rm.fyf - p.yf, rm.fxf - p.xf);
+            const float b = at - p.rotYf;
+            cph = cosf(b + (float)kHalfPI);
         }
-        amb |= !(fabs(norm) >= 1e-3);
-        const double v = on ? fmin(fabs((double)th - rc.amin), fabs((double)th - rc.amax)) / norm
-                            : 0.0;
-        rang = v;
-        eang = (float)((double)(2.0f * kDeltaTh) / fabs(norm)) + 4.0f * U * (float)fabs(v);
+        if (rel) {
+            const RelConst& rc = ch.relc[i];
+            const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
+            const ObjP as = ch.P[rc.as], atp = ch.P[rc.at];
+            rpw = rel_pw_est(rc, ps, pt, amb);
+            rang = rel_ang_est(rc, atp, atan2f(as.yf - atp.yf, as.xf - atp.xf),
+                               as.xf - atp.xf, as.yf - atp.yf, eang, amb);
+        }
+        return;
     }
+    // One atan2f pass serves a relationship lane's angle (theta) or, failing that, an object
+    // lane's focal angle; a lane needing both (its object moved and its relationship was touched)
+    // takes a second pass (config 3: 115.2 -> 114.4 ms per launch).
+    const ObjP p = ch.P[i < n ? i : 0];
+    const float fy = rm.fyf - p.yf, fx = rm.fxf - p.xf;
+    float ay = fy, ax = fx;
+    const RelConst* rc = nullptr;
+    ObjP atp;
+    if (rel) {
+        rc = &ch.relc[i];
+        const ObjP ps = ch.P[rc->s], pt = ch.P[rc->t];
+        rpw = rel_pw_est(*rc, ps, pt, amb);
+        const ObjP as = ch.P[rc->as];
+        atp = ch.P[rc->at];
+        ay = as.yf - atp.yf;
+        ax = as.xf - atp.xf;
+    }
+    const float a1 = atan2f(ay, ax);
+    float at = a1;
+    if (obj && rel) at = atan2f(fy, fx);
+    if (obj) cph = cosf((at - p.rotYf) + (float)kHalfPI);
+    if (rel) rang = rel_ang_est(*rc, atp, a1, ax, ay, eang, amb);
 }
 
 // ---- incremental Clearance pairs (one object per lane) ---------------------------------------
@@ -291,7 +319,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
 // carry; the others keep their zero / non-zero state. Updates this lane's column mask and the
 // proposed row words (the other LDS buffer), writes the row prefix counts of the proposed rows
 // and returns the number of non-zero pairs (Kernel.cu:408-431 terms that are not exactly zero).
-template <int L, bool HOIST = false>
+template <int L>
 __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, int ka, int kb,
                                              int r, int gbase, float4 boxj, const ClPairs& clp,
                                              ClPairs& clo, bool& colchg) {
@@ -313,8 +341,8 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
         w = (w & ~(1ull << k)) | ((uint64_t)nzk << k);
     }
     // rows of the clearances whose source moved: every object lane re-tests its pair
-    const int src = r < c ? (HOIST ? ch.lc.pad : ch.clrs[r].pad) : -2;
-    uint64_t moved = group_ballot<L>(src == ka || src == kb, gbase);
+    uint64_t moved = group_ballot<L>(r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb),
+                                     gbase);
     while (moved) {
         const int i = __builtin_ctzll(moved);
         moved &= moved - 1;
@@ -374,7 +402,6 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // latency-bound step; config 2 4.30 -> 4.25 ms per 1,000-step launch)
     const DevRoom& rm = PAIRS ? a.rm : *ch.rm;
     const int n = a.rm.n, c = a.rm.c;
-    constexpr bool HOIST = PAIRS && MH_HOIST_FEW;  // (lane r's room records in registers)
 
     unsigned long long t0 = 0;
     MH_STAMP(t0);
@@ -406,7 +433,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const bool moved = i < n && (i == ka || i == kb) && !(MH_ABLATE & 2);
             bool touched = false;
             if (i < rm.r && !(MH_ABLATE & 16)) {
-                const uint2 q = HOIST ? ch.lx : ch.rix[i];
+                const uint2 q = ch.rix[i];
                 const unsigned a16 = (unsigned)ka, b16 = (unsigned)kb;  // (ka, kb < 65536)
                 touched = ka >= 0 && ((q.x & 0xffffu) == a16 || (q.x >> 16) == a16 ||
                                       (q.y & 0xffffu) == a16 || (q.y >> 16) == a16 ||
@@ -422,7 +449,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             if constexpr (FAST) {
                 bool amb = false;
                 if (__ballot(moved || touched))
-                    approx_terms<HOIST>(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
+                    approx_terms<!PAIRS>(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
                                  amb);
                 clo.dc = clo.dc || moved;
                 clo.dr = clo.dr || touched;
@@ -431,28 +458,20 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                         clo.dr = false;
                         clo.eang = 0.0f;
                     }
-                    exact_terms<HOIST>(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
+                    exact_terms(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
                 }
             } else {
                 const bool obj = moved || (i < n && clp.dc);
                 const bool rel = touched || (i < rm.r && clp.dr);
-                if (__ballot(obj || rel))
-                    exact_terms<HOIST>(ch, rm, i, n, obj, rel, cph[m], rpw[m], rang[m]);
+                if (__ballot(obj || rel)) exact_terms(ch, rm, i, n, obj, rel, cph[m], rpw[m], rang[m]);
                 clo.dc = clo.dr = false;
                 clo.eang = 0.0f;
             }
         }
         if (i < n) {
-            const RectShape os = HOIST ? ch.lo : ch.objs[i];
+            const RectShape os = ch.objs[i];
             const float area = __int_as_float(os.pad);
-            ObjP p;
-            if constexpr (HOIST) {  // (the float pose words are the registers' poses rounded)
-                p.xf = (float)op.x[m];
-                p.yf = (float)op.y[m];
-                p.rotYf = (float)op.ry[m];
-            } else {
-                p = ch.P[i];
-            }
+            const ObjP p = ch.P[i];
             const double x = op.x[m], y = op.y[m];
             wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(op.ry[m]) < 1e15);
             // VisualBalanceCosts products, Kernel.cu:200-201.
@@ -494,7 +513,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             }
         }
         if (i < c) {
-            const RectShape cs = HOIST ? ch.lc : ch.clrs[i];
+            const RectShape cs = ch.clrs[i];
             const ObjP ps = ch.P[cs.pad];
             ch.CLA[i] = shape_box(cs, ps.xf, ps.yf);             // ClearanceCosts, :414-415
         }
@@ -506,14 +525,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             sa_new = sa_new && (i == ka || i == kb);
         }
         if (sa_new) {
-            ObjP pi;
-            if (HOIST && i < n) {  // (a clearance past the objects reads the pose words as before)
-                pi.xf = (float)op.x[m];
-                pi.yf = (float)op.y[m];
-            } else {
-                pi = ch.P[i];
-            }
-            sac[m] = comp_overlaps(rm, shape_box(HOIST ? ch.lc : ch.clrs[i], pi.xf, pi.yf));
+            const ObjP pi = ch.P[i];
+            sac[m] = comp_overlaps(rm, shape_box(ch.clrs[i], pi.xf, pi.yf));
         }
         if constexpr (NPL == 1) clo.sac = sac[0];
     }
@@ -842,8 +855,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             MH_CLOBBER();
             colchg = colchg0;
 #endif
-            cl_total = inc_cl_update<L, HOIST>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo,
-                                               colchg);
+            cl_total = inc_cl_update<L>(ch, n, c, ka, kb, r, gbase, boxo[0], clp, clo, colchg);
 #if MH_DOUBLE & 128
         }
 #endif
@@ -953,7 +965,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             if (__ballot(obj || rel)) {
                 float c0 = cph[0];
                 double p0 = rpw[0], a0 = rang[0];
-                exact_terms<HOIST>(ch, rm, r, n, obj, rel, c0, p0, a0);
+                exact_terms(ch, rm, r, n, obj, rel, c0, p0, a0);
 #if MH_CHECK
                 // the estimates' allowances, against the exact values
                 MH_CK(!obj || fabsf(cph[0] - c0) <= kDeltaCph, 30, __float_as_uint(cph[0]),
@@ -1510,12 +1522,6 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
     ch.zero4 = reinterpret_cast<const double*>(lds + F.h_zero);
-    if constexpr (OP == OP_STEP_FEW && MH_HOIST_FEW) {
-        ch.lo = objs_l[r < n ? r : 0];
-        ch.lc = clrs_l[r < a.rm.c ? r : 0];
-        ch.lr = relc_l[r < a.rm.r ? r : 0];
-        ch.lx = rix_l[r < a.rm.r ? r : 0];
-    }
 
     // Zero the dense replay streams past N (never written afterwards).
     for (int i = n + r; i < a.lay.N4; i += L) {
