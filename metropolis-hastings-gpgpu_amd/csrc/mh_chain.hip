@@ -1398,17 +1398,19 @@ __device__ __forceinline__ void commit_swap_zrr(const ChainPtrs& ch, int n) {
     }
 }
 
-// Undo the last proposal (every lane of the group; the backups are group-uniform LDS reads).
+// Undo the last proposal (every lane of the group; the backups are group-uniform LDS reads),
+// knowing which objects it changed (kk, as propose returned it: a swap of an object with itself
+// restores only b[0], which holds the same original pose as b[1]). Both backups are read at once
+// instead of after the count (config 3 114.5 -> 113.8 ms, config 2 4.24 -> 4.20 ms per launch).
 template <int L, int NPL>
 __device__ __forceinline__ void restore(const ChainPtrs& ch, OwnPose<NPL>& op, int r,
-                                        bool writer) {
-    const int nb = ch.aux->nb;
-    if (!MH_CK(nb >= 0 && nb <= 2, 2, nb, 0)) return;
-    for (int q = nb - 1; q >= 0; --q) {
-        const Backup b = ch.aux->b[q];
-        if (!MH_CK(b.k >= 0 && b.k < ch.rm->n, 3, b.k, q)) continue;
-        write_obj<L, NPL>(ch, op, r, writer, b.k, b.x, b.y, b.ry);
-    }
+                                        bool writer, int2 kk) {
+    const Backup b1 = ch.aux->b[1];
+    const Backup b0 = ch.aux->b[0];
+    if (kk.y >= 0 && MH_CK(b1.k == kk.y, 3, b1.k, kk.y))
+        write_obj<L, NPL>(ch, op, r, writer, b1.k, b1.x, b1.y, b1.ry);
+    if (kk.x >= 0 && MH_CK(b0.k == kk.x, 2, b0.k, kk.x))
+        write_obj<L, NPL>(ch, op, r, writer, b0.k, b0.x, b0.y, b0.ry);
 }
 
 // ---- the kernel ---------------------------------------------------------------------------
@@ -1693,7 +1695,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                           k0 | (nb << 16), k1);
                     const Backup s0 = read_obj<L, NPL>(op, k0, gbase);
                     const Backup s1 = read_obj<L, NPL>(op, k1, gbase);
-                    restore<L, NPL>(ch, op, r, writer);
+                    restore<L, NPL>(ch, op, r, writer, kk);
                     wave_sync();
                     float cx[8];
                     SymRows<NPL> sx;
@@ -1720,7 +1722,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 #endif
                     wave_sync();
                     if (u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total))) {
-                        restore<L, NPL>(ch, op, r, writer);  // the proposal again
+                        restore<L, NPL>(ch, op, r, writer, kk);  // the proposal again
                         fast = BOUND_ACCEPT + 1;  // accepted with exact costs (below)
                     } else {
                         fast = BOUND_REJECT + 16;  // rejected, already undone
@@ -1769,7 +1771,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     commit_swap_zrr(ch, n);
                 }
             } else if (fast != BOUND_REJECT + 16) {
-                restore<L, NPL>(ch, op, r, writer);
+                restore<L, NPL>(ch, op, r, writer, kk);
             }
             wave_sync();
             if (writer) MH_PHASE(ch, 7, ts);
