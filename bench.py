@@ -75,22 +75,40 @@ def combine_records(recs):
             "accepted": int(sum(r[4] for r in recs))}
 
 
+def cpu_share():
+    """(CPUs this job may use, where that number comes from): the cgroup's CPU quota
+    (/sys/fs/cgroup/cpu.max, cgroup v2) when one is set, else $OMP_NUM_THREADS (the GPU pool sets
+    it to the one-GPU job's share), else 16."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period))), f"cgroup cpu.max {quota} {period}"
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env), f"OMP_NUM_THREADS={env}"
+    return 16, "default (16)"
+
+
 def host_cores():
-    """(threads the CPU baseline uses, nproc, CPUs this process may run on). The GPU box grants
-    a one-GPU job a 16-CPU share of a larger machine whose CPUs nproc counts in full, so the
-    baseline runs on min(affinity, 16) threads and reports all three numbers."""
+    """(threads the CPU baseline uses, nproc, CPUs this process may run on, share source). The
+    GPU box grants a one-GPU job a share of a larger machine whose CPUs nproc and the affinity
+    mask count in full, so the baseline runs on min(affinity, share) threads (cpu_share) and
+    reports every number."""
     nproc = os.cpu_count() or 1
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
-    return max(1, min(affinity, 16)), nproc, affinity
+    share, source = cpu_share()
+    return max(1, min(affinity, share)), nproc, affinity, source
 
 
 def cpu_baseline(room, orc, seed: int, budget_s: float):
     """Oracle chain (the reference's algorithm, Kernel.cu:777-828, OffLimits included as the
     reference computes it every step) on the host's cores, bounded to ~budget_s."""
-    threads, nproc, affinity = host_cores()
+    threads, nproc, affinity, source = host_cores()
     t0 = time.perf_counter()
     orc.run_chains(room, threads, 20, seed, threads=threads)
     per = (time.perf_counter() - t0) / (threads * 20) * threads  # seconds per chain-step/thread
@@ -101,9 +119,10 @@ def cpu_baseline(room, orc, seed: int, budget_s: float):
     dt = time.perf_counter() - t0
     return {"value": chains * steps / dt, "unit": "chain-steps/s", "cores": threads,
             "kind": "port", "host_nproc": nproc, "host_affinity_cpus": affinity,
+            "cpu_share_source": source,
             "sample": f"oracle/mh_oracle.c chain on {room.name}: {chains} chains x {steps} steps"
                       f" ({dt:.1f} s, {threads} threads; nproc {nproc}, {affinity} CPUs in this"
-                      f" process's affinity, 16 of them the box's per-GPU share)"}
+                      f" process's affinity; the job's CPU share from {source})"}
 
 
 def e2e_wrapper(mh, room, chains: int, iters: int, seed: int):
