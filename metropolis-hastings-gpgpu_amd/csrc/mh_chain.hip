@@ -61,6 +61,8 @@ struct ChainAux {
     int nb;       // backups in use (0, 1 or 2)
     int swap_a, swap_b;  // a swap proposal's objects (-1: none); z/rotX/rotZ swap in HBM on accept
     float cur[8]; // resultCosts of the current configuration
+    uint64_t rng_key[3];  // the Philox stream's seed and subsequence, the window's first draw
+                          // (WaveRngLds::ss)
 #if MH_STAMPS
     unsigned long long cyc[12];  // diagnostic: cycles per phase (writer lane); [8] steps that
                                  // evaluated the bound, [9] steps it rejected, [10] steps it
@@ -1592,10 +1594,15 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         float chk_cur = cur_total;  // (check builds: the current total, always exact)
 #endif
         Rng rng;
-        if constexpr (std::is_same<Rng, WaveRngLds>::value)
+        if constexpr (std::is_same<Rng, WaveRngLds>::value) {
             rng.bsl = reinterpret_cast<float*>(base + F.RNG);
+            rng.ss = ch.aux->rng_key;
+        }
         rng_load(rng, a, chain, m0);
-        uint64_t accepted = m0.accepted;
+        // This launch's accepted count (at most `iterations`); the meta record's count, rung and
+        // best total are re-read at the end rather than kept in scalar registers across the
+        // steps (config 2 4.01 -> 3.93 ms per launch together with WaveRngLds's offset).
+        unsigned int accepted = 0;
         float best_total = m0.best_total;
         double beta = kBeta;
         if constexpr (TRACK)  // (the extended families also carry parallel tempering)
@@ -1798,14 +1805,15 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 #endif
         if (writer) {
             ChainMeta m;
-            m.draws = rng.draws;
-            m.accepted = accepted;
+            const ChainMeta m1 = a.meta[chain];  // (re-read: m0 need not stay live)
+            m.accepted = m1.accepted + accepted;
+            m.draws = rng_draws(rng);
             m.bm_has = rng.bm_has;
             m.bm_val = rng.bm_val;
             rng_save(rng, a, chain);
             for (int k = 0; k < 8; ++k) m.costs[k] = ch.aux->cur[k];
-            m.best_total = best_total;
-            m.rung = m0.rung;
+            m.best_total = TRACK ? best_total : m1.best_total;
+            m.rung = m1.rung;
             if (MH_CK(chain >= 0 && chain < a.n_chains, 12, (unsigned)chain, 0)) a.meta[chain] = m;
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits

@@ -313,30 +313,39 @@ struct WaveRng {
 // two registers per lane: the full-evaluation step kernel is held to 96 VGPRs, and the pairs it
 // kept in registers were spilled to scratch at every window fill.
 struct WaveRngLds {
-    uint64_t seed, subseq;
-    uint64_t base;   // first draw of the window
-    uint64_t draws;  // next draw
-    unsigned int w;  // lane i: word base + i
-    float* bsl;      // [i], [64 + i]: box_muller(word base + i, word base + i + 1)
+    // The stream's key and the window's first draw in LDS (ss[0] = seed, ss[1] = subsequence,
+    // ss[2] = window start), read only at a window fill or a draw past the window; the step
+    // carries only the 32-bit offset of the next draw in the window. The step kernel spills
+    // scalar registers into vector lanes (v_writelane / v_readlane): the key out of scalar
+    // registers took config 3 from 113.6 to 112.0 ms per launch, the offset for the 64-bit draw
+    // count and window start from 111.7 to 110.3 ms (config 2 4.20 -> 4.01 ms with both).
+    uint64_t* ss;
+    __device__ __forceinline__ uint64_t seed_() const { return ss[0]; }
+    __device__ __forceinline__ uint64_t subseq_() const { return ss[1]; }
+    unsigned int off;  // next draw - window start
+    unsigned int w;    // lane i: word (window start) + i
+    float* bsl;        // [i], [64 + i]: box_muller(word start + i, word start + i + 1)
     int bm_has;
     float bm_val;
 
+    __device__ __forceinline__ uint64_t draws() const { return ss[2] + off; }
     __device__ __forceinline__ void fill(uint64_t at) {
-        base = at;
-        const WaveWindow ww = wave_window(seed, subseq, at);
+        ss[2] = at;  // (every lane stores the same value)
+        off = 0;
+        const WaveWindow ww = wave_window(seed_(), subseq_(), at);
         w = ww.w;
         const int lane = __lane_id();
         bsl[lane] = ww.bs;
         bsl[64 + lane] = ww.bc;
     }
     __device__ __forceinline__ void prepare() {
-        if (draws - base > 64 - 16) fill(draws);
+        if (off > 64 - 16) fill(ss[2] + off);
     }
-    __device__ __forceinline__ unsigned int word_at(uint64_t d) const {
-        if (d - base < 64) return (unsigned int)__builtin_amdgcn_readlane((int)w, (int)(d - base));
-        return philox_word(seed, subseq, d);
+    __device__ __forceinline__ unsigned int word_off(unsigned int o) const {
+        if (o < 64) return (unsigned int)__builtin_amdgcn_readlane((int)w, (int)o);
+        return philox_word(seed_(), subseq_(), ss[2] + o);
     }
-    __device__ __forceinline__ unsigned int next() { return word_at(draws++); }
+    __device__ __forceinline__ unsigned int next() { return word_off(off++); }
     __device__ __forceinline__ float uniform() {
         return rocrand_device::detail::uniform_distribution(next());
     }
@@ -346,21 +355,23 @@ struct WaveRngLds {
             return bm_val;
         }
         float zs, zc;
-        if (draws - base < 63) {
-            const int i = (int)(draws - base);
-            zs = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[i])));
-            zc = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[64 + i])));
+        if (off < 63) {
+            zs = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[off])));
+            zc = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bsl[64 + off])));
         } else {
-            const float2 z = box_muller_inl(word_at(draws), word_at(draws + 1));
+            const float2 z = box_muller_inl(word_off(off), word_off(off + 1));
             zs = z.x;
             zc = z.y;
         }
-        draws += 2;
+        off += 2;
         bm_val = zc;
         bm_has = 1;
         return zs;
     }
 };
+
+template <class R> __device__ __forceinline__ uint64_t rng_draws(const R& r) { return r.draws; }
+__device__ __forceinline__ uint64_t rng_draws(const WaveRngLds& r) { return r.draws(); }
 
 template <bool XW, int L = 0> struct RngOf { using type = ChainRng; };
 template <> struct RngOf<false, 64> { using type = WaveRng; };
@@ -404,9 +415,8 @@ __device__ __forceinline__ void rng_prepare(WaveRngLds& r) { r.prepare(); }
 // (bsl must be set before the load: the first window is filled here)
 __device__ __forceinline__ void rng_load(WaveRngLds& r, const LaunchArgs& a, int64_t chain,
                                          const ChainMeta& m) {
-    r.seed = a.seed;
-    r.subseq = (uint64_t)(a.chain_offset + chain);
-    r.draws = m.draws;
+    r.ss[0] = a.seed;  // (every lane stores the same values)
+    r.ss[1] = (uint64_t)(a.chain_offset + chain);
     r.bm_has = m.bm_has;
     r.bm_val = m.bm_val;
     r.fill(m.draws);
@@ -911,15 +921,19 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     // VisualBalanceCosts (Kernel.cu:191-207): -|(nx/denom, ny/denom) - centroid/2|
     const float id = fabsf(rm.inv_denom);
     const float cv = (n + 26.0f + kf) * U;  // (float accumulators, Kernel.cu:200-201)
-    const float enx = cv * a_nx * id, eny = cv * a_ny * id;
+    // The chain of the reference's roundings below -- (enx + eny) = S for the two sums, 3 U on
+    // ad, bd (the division), 2 U on fx, fy (the centroid subtraction), 2 U on the distance, 3 U
+    // on the weight product -- composed with each (1 + kU) factor expanded: the exact error of
+    // w_vb vb is at most |w_vb| (S (1 + 11 U) + 3.01 U A + 2.01 U F + 6 U |vb|), A = |ad| + |bd|,
+    // F = |fx| + |fy|; written with 32 U, 4 U, 4 U and 8 U to absorb this expression's own roundings.
+    const float S = cv * id * (a_nx + a_ny);
     const float ad = s_nx * rm.inv_denom, bd = s_ny * rm.inv_denom;
-    const float da = enx + 3.0f * U * (fabsf(ad) + enx), db = eny + 3.0f * U * (fabsf(bd) + eny);
     const float fx = ad - rm.cxf, fy = bd - rm.cyf;
-    const float dfx = da + 2.0f * U * (fabsf(fx) + da), dfy = db + 2.0f * U * (fabsf(fy) + db);
     const float vb = -__builtin_sqrtf(fx * fx + fy * fy);
-    const float dvb = dfx + dfy + 2.0f * U * (fabsf(vb) + dfx + dfy);
     const float o2 = rm.w_vb * vb;
-    const float e2 = fabsf(rm.w_vb) * (dvb + 3.0f * U * (fabsf(vb) + dvb));
+    const float e2 = fabsf(rm.w_vb) *
+                     (S * (1.0f + 32.0f * U) +
+                      4.0f * U * ((fabsf(ad) + fabsf(bd)) + (fabsf(fx) + fabsf(fy)) + 2.0f * fabsf(vb)));
     // PairWise x PairWiseAngle (Kernel.cu:518), both sums accumulated in double (:222, :249-253)
     float pa, dpa;
     if constexpr (DPW) {
