@@ -330,7 +330,9 @@ struct WaveRngLds {
 
     __device__ __forceinline__ uint64_t draws() const { return ss[2] + off; }
     __device__ __forceinline__ void fill(uint64_t at) {
-        ss[2] = at;  // (every lane stores the same value)
+        ss[2] = at;  // (every lane stores the same value: a store by one lane would need a
+                     // wave_sync before the others read it, or the compiler forwards each
+                     // lane's stale value -- measured as forked chains)
         off = 0;
         const WaveWindow ww = wave_window(seed_(), subseq_(), at);
         w = ww.w;
