@@ -1520,9 +1520,14 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
     ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
-    ch.CLA = reinterpret_cast<float4*>(base + a.lay.CLA);
-    ch.NZ = reinterpret_cast<uint64_t*>(base + a.lay.NZ);
-    ch.PRE = reinterpret_cast<int*>(base + a.lay.PRE);
+    {
+        constexpr int kCla = fixed_cla(F);
+        const int c1 = a.rm.c > 0 ? a.rm.c : 1;
+        MH_CK(a.lay.CLA == kCla && a.lay.NZ == kCla + 16 * c1, 13, a.lay.CLA, kCla);
+        ch.CLA = reinterpret_cast<float4*>(base + kCla);
+        ch.NZ = reinterpret_cast<uint64_t*>(base + kCla + 16 * c1);
+        ch.PRE = reinterpret_cast<int*>(base + kCla + 32 * c1);
+    }
     ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
     ch.rm = rm_l;
     ch.zero4 = reinterpret_cast<const double*>(lds + F.h_zero);
