@@ -145,22 +145,35 @@ def e2e_wrapper(mh, room, chains: int, iters: int, seed: int):
             "note": "host buffers in, host result out (PCIe both ways); never `value`"}
 
 
-def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str):
-    """The committed rocprofv3 PMC record of the step kernel (profiles/pmc_step_kernel_n<N>.json,
-    written by tools/pmc_summary.py --json) if it was taken on this workload, else {}."""
+def library_srchash(mh) -> str | None:
+    """The source hash recorded next to the library this process loaded (None for a library
+    without one, e.g. an ablate/ variant under $MH_LIB)."""
+    lib = Path(os.environ.get("MH_LIB", mh.LIB_PATH))
+    stamp = lib.with_name(lib.name + ".srchash")
+    return stamp.read_text().strip() if stamp.exists() else None
+
+
+def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str, srchash: str | None):
+    """(record, status): the committed rocprofv3 PMC record of the step kernel
+    (profiles/pmc_step_kernel_n<N>.json, written by tools/pmc_summary.py --json) if it was taken
+    on this workload AND on a library built from the same sources as the one loaded (its srchash
+    stamp), else {} -- a PMC record of another build never describes this one."""
     p = ROOT / "profiles" / f"pmc_step_kernel_n{n}.json"
     if not p.exists():
-        return {}
+        return {}, "no PMC record for this room"
     try:
         d = json.loads(p.read_text())
-        k = d.get("kernel", "")
-        kind = ("incremental" if "delta" in k else
-                "full-few" if "mh_kernel<64, 1, 6>" in k else "full")
-        if int(d.get("chains_per_launch", -1)) != n_chains_per_launch or kind != step_kernel:
-            return {}
-        return d
-    except Exception:
-        return {}
+    except Exception as e:  # noqa: BLE001
+        return {}, f"unreadable PMC record ({e})"
+    k = d.get("kernel", "")
+    kind = ("incremental" if "delta" in k else
+            "full-few" if "mh_kernel<64, 1, 6>" in k else "full")
+    if int(d.get("chains_per_launch", -1)) != n_chains_per_launch or kind != step_kernel:
+        return {}, "PMC record of another workload"
+    if not srchash or d.get("srchash") != srchash:
+        return {}, (f"stale: PMC record of library {str(d.get('srchash'))[:12]}, this library "
+                    f"{str(srchash)[:12]}")
+    return d, f"current (library {srchash[:12]})"
 
 
 CONFIG_NAMES = {(64, 65536): "config 3: ", (256, 32768): "config 5: ", (8, 1024): "config 2: "}
@@ -194,6 +207,11 @@ def main() -> int:
     # One process per GPU over RCCL. $MH_BENCH_BACKEND=gloo rehearses the multi-rank path on a
     # box with fewer GPUs than ranks (ranks then share devices round-robin; CPU-side collectives).
     backend = os.environ.get("MH_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and world > 1 and torch.cuda.device_count() < world:
+        # (one process per GPU: fewer visible GPUs than ranks would fail inside RCCL later)
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, this process sees "
+                         f"{torch.cuda.device_count()} (MH_BENCH_BACKEND=gloo rehearses the "
+                         f"multi-rank path on fewer GPUs)")
     device = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
@@ -278,7 +296,7 @@ def main() -> int:
         if world == 1 and not args.no_cpu_baseline:
             orc = graft.load_oracle()
             cpu = cpu_baseline(room, orc, args.seed, args.cpu_budget)
-        pmc = pmc_record(n, args.chains, step_kernel)
+        pmc, pmc_status = pmc_record(n, args.chains, step_kernel, library_srchash(mh))
         out = {
             "metric": f"MH chain-steps/sec (whole node) + mean final cost, N={n} objects",
             "value": value,
@@ -333,6 +351,8 @@ def main() -> int:
                 # the tracked record this block reads, and the counter summary it was made from
                 "pmc_source": (f"profiles/pmc_step_kernel_n{n}.json" if pmc else None),
                 "pmc_profile": pmc.get("profile"),
+                "pmc_srchash": pmc.get("srchash"),
+                "pmc_status": pmc_status,
             },
             "cpu_baseline": cpu,
             "e2e_chain_steps_per_s": e2e["chain_steps_per_s"] if e2e else None,

@@ -291,6 +291,13 @@ MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int
 MH_API int mh_debug_rng_ex(int rng, uint64_t seed, uint64_t subsequence, int n,
                            unsigned int* out_u32, float* out_uniform, float* out_normal);
 
+/* The project's transcendentals (metropolis-hastings-gpgpu_amd/csrc/mh_math.h, shared with the
+ * test oracle) evaluated on the current device by the device code the chains use: probe `fn`
+ * (MH_PROBE_* in mh_math.h: the Box-Muller log and sincos, cosf, cuRAND's log and sincos, atan2,
+ * atan2f and exp on the chains' argument streams) at argument indices start .. start + count - 1
+ * (count <= 2^28); out receives count x width doubles (width 2 for the sincos probes). */
+MH_API int mh_debug_math(int fn, uint64_t start, uint64_t count, double* out);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

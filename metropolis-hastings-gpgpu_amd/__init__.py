@@ -7,6 +7,7 @@ bench use. The directory name contains hyphens, so load it with load_package() b
 importlib) rather than a plain import.
 """
 from .abi import (COST_FIELDS, EXPORTS, LIB_PATH, MHError, Room, Session, STRUCT_LAYOUT,  # noqa: F401
-                  debug_collectives, debug_rng, evaluate_costs, kernel_wrapper, last_error,
+                  debug_collectives, debug_math, debug_rng, evaluate_costs, kernel_wrapper,
+                  last_error,
                   load_library)
 from .rooms import clone_cfg, main_fixture, synthetic_room  # noqa: F401

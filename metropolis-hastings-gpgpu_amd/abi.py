@@ -125,7 +125,8 @@ EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelWrapperEx", "KernelFre
            "mh_session_run", "mh_session_finalize",
            "mh_session_download", "mh_session_current_costs", "mh_session_summary",
            "mh_session_geometry", "mh_session_occupancy",
-           "mh_session_destroy", "mh_debug_rng", "mh_debug_rng_ex", "mh_debug_collectives"]
+           "mh_session_destroy", "mh_debug_rng", "mh_debug_rng_ex", "mh_debug_collectives",
+           "mh_debug_math"]
 
 P = C.POINTER
 
@@ -211,6 +212,9 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_debug_rng_ex.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, P(C.c_uint32),
                                     P(C.c_float), P(C.c_float)]
     lib.mh_debug_rng_ex.restype = C.c_int
+    if hasattr(lib, "mh_debug_math"):  # (A/B variants of earlier revisions lack it)
+        lib.mh_debug_math.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_void_p]
+        lib.mh_debug_math.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -323,6 +327,16 @@ def debug_rng(seed: int, subsequence: int, n: int, rng: int = MH_RNG_PHILOX):
     return (np.frombuffer(bytes(u), dtype=np.uint32).copy(),
             np.frombuffer(bytes(f), dtype=np.float32).copy(),
             np.frombuffer(bytes(g), dtype=np.float32).copy())
+
+
+def debug_math(fn: int, start: int, count: int, width: int) -> np.ndarray:
+    """mh_debug_math: the shared transcendentals' probe `fn` evaluated on the device, float64
+    [count, width] (diagnostic; tests/test_gpu_math.py)."""
+    lib = load_library()
+    out = np.empty((count, width), dtype=np.float64)
+    if lib.mh_debug_math(fn, C.c_uint64(start), C.c_uint64(count), out.ctypes.data) != 0:
+        raise MHError(last_error(lib))
+    return out
 
 
 def debug_collectives(L: int, v, iv):

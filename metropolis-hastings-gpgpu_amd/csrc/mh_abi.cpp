@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "mh_launch.h"
+#include "mh_math.h"
 
 static_assert((int)mh::RNG_PHILOX == MH_RNG_PHILOX &&
                   (int)mh::RNG_CURAND_XORWOW == MH_RNG_CURAND_XORWOW, "RNG kinds");
@@ -139,8 +140,8 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
     rm.w_sa = srf->WeightSurfaceArea;
     rm.fxf = (float)srf->focalX;
     rm.fyf = (float)srf->focalY;
-    rm.ux = (float)cos(srf->focalRot);  // Kernel.cu:290
-    rm.uy = (float)sin(srf->focalRot);  // Kernel.cu:291
+    rm.ux = (float)mh_cos(srf->focalRot);  // Kernel.cu:290 (mh_math.h, as the oracle)
+    rm.uy = (float)mh_sin(srf->focalRot);  // Kernel.cu:291
     rm.cxf = (float)(srf->centroidX / 2);
     rm.cyf = (float)(srf->centroidY / 2);
     double along = srf->focalX * rm.ux;
@@ -266,7 +267,10 @@ void choose_delta_geometry(int n, int c, int r, int max_lds, Geometry& g) {
     if (g.dwaves == 0 || best_chains <= 0) g.delta = false;  // does not fit: full evaluation
 }
 
-bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, Geometry& g) {
+// `plain`: the session runs the plain step family (no best-of-chain tracking, no tempering, the
+// Philox stream); only that family has the few-chains instance (launch() sends the others to
+// launch_step_best / launch_step_xw).
+bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool plain, Geometry& g) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1)
         cus = 256;
@@ -294,9 +298,9 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, Geometry
     // At most two chains per SIMD: the step kernel's register cap (five resident waves per SIMD)
     // buys nothing, and its spills lengthen every step (config 2: 1.92e8 chain-steps/s uncapped
     // against 1.77e8). $MH_STEP_FEW=0/1 forces the choice.
-    g.few = g.L == 64 && g.npl <= 1 && n_chains <= 8LL * cus;
+    g.few = plain && g.L == 64 && g.npl <= 1 && n_chains <= 8LL * cus;
     if (const char* e = getenv("MH_STEP_FEW"))
-        if (*e) g.few = g.L == 64 && g.npl <= 1 && atoi(e) != 0;
+        if (*e) g.few = plain && g.L == 64 && g.npl <= 1 && atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
     g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
@@ -473,7 +477,9 @@ bool session_init(mh_session* s) {
     MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     MH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
     s->last = s->stream;
-    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->n_chains, s->geo))
+    const bool plain = s->track == mh::TRACK_OFF && s->n_temps <= 1 && s->rng == mh::RNG_PHILOX;
+    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->n_chains, plain,
+                         s->geo))
         return false;
     if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
@@ -539,17 +545,24 @@ bool session_finalize(mh_session* s, hipStream_t st) {
     return record_done(s, st);
 }
 
-// Copies `bytes` from device memory into a caller's (pageable) host buffer on the session's
-// stream, ordered after the session's work: the host range is page-locked for the copy so the
-// DMA runs straight into it and does not serialise against other devices' work (KernelWrapper
-// runs one host thread per device); where it cannot be locked, a plain staged copy.
-bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes) {
+// $MH_DOWNLOAD_PAGEABLE=1: downloads never page-lock the caller's buffer (the staged copy only,
+// for the A/B of the two).
+bool download_pageable() {
+    static const bool pageable = getenv("MH_DOWNLOAD_PAGEABLE") && atoi(getenv("MH_DOWNLOAD_PAGEABLE"));
+    return pageable;
+}
+
+// Copies `bytes` from device memory into a caller's host buffer on the session's stream, ordered
+// after the session's work. Unless `locked_by_caller` (KernelWrapper page-locks its whole result
+// once, before its per-device threads start: shards of one buffer share boundary pages, which
+// two threads must not lock and unlock independently), the host range is page-locked for the
+// copy so the DMA runs straight into it; where it cannot be locked, a plain staged copy.
+bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes, bool locked_by_caller) {
     if (bytes == 0) return true;
     hipStream_t st = s->stream;
     if (!order_after_last(s, st)) return false;
-    // ($MH_DOWNLOAD_PAGEABLE=1: the staged copy only, for the A/B of the two)
-    static const bool pageable = getenv("MH_DOWNLOAD_PAGEABLE") && atoi(getenv("MH_DOWNLOAD_PAGEABLE"));
-    const bool locked = !pageable && hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
+    const bool locked = !locked_by_caller && !download_pageable() &&
+                        hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
     if (!locked) (void)hipGetLastError();  // (clear the sticky error of the failed lock)
     MH_TRY_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
     const hipError_t e = hipStreamSynchronize(st);
@@ -560,13 +573,23 @@ bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes) {
 
 // The session's final points and costs, after all of its queued work (an event wait, so another
 // session's work on the same device is not waited for).
-bool session_download(mh_session* s, point* pts, resultCosts* costs) {
+bool session_download(mh_session* s, point* pts, resultCosts* costs, bool locked_by_caller = false) {
     MH_TRY_HIP(hipSetDevice(s->device));
     const size_t n = (size_t)s->room.rm.n;
     if (s->n_chains <= 0) return true;
-    if (pts && !copy_out(s, pts, s->d_pts, sizeof(point) * n * s->n_chains)) return false;
-    if (costs && !copy_out(s, costs, s->d_costs, sizeof(resultCosts) * s->n_chains)) return false;
+    if (pts && !copy_out(s, pts, s->d_pts, sizeof(point) * n * s->n_chains, locked_by_caller))
+        return false;
+    if (costs && !copy_out(s, costs, s->d_costs, sizeof(resultCosts) * s->n_chains, locked_by_caller))
+        return false;
     return true;
+}
+
+// Page-locks a host range for every device (portable), or leaves it pageable (false).
+bool lock_host(void* p, size_t bytes) {
+    if (bytes == 0 || download_pageable()) return false;
+    if (hipHostRegister(p, bytes, hipHostRegisterPortable) == hipSuccess) return true;
+    (void)hipGetLastError();  // (clear the sticky error of the failed lock)
+    return false;
 }
 
 mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
@@ -600,32 +623,52 @@ mh_session* session_create(const Room& room, int device, int64_t n_chains, int64
     return s;
 }
 
-std::vector<int> devices_from_env(int current) {
-    std::vector<int> d;
+// The devices a KernelWrapper call shards over: $MH_DEVICES ("all", or a comma list of device
+// ids), else the current device. Unknown ids are an error, and so is a repeated id -- two shards
+// on one device are not a multi-GPU run -- unless $MH_DEVICES_ALLOW_DUPLICATES=1 (the one-GPU
+// test of the sharding path).
+bool devices_from_env(int current, std::vector<int>& d) {
+    d.clear();
     const char* s = getenv("MH_DEVICES");
     if (!s || !*s) {
         d.push_back(current);
-        return d;
+        return true;
     }
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
     if (strcmp(s, "all") == 0) {
         for (int i = 0; i < count; ++i) d.push_back(i);
     } else {
+        const char* dup = getenv("MH_DEVICES_ALLOW_DUPLICATES");
+        const bool allow_dup = dup && atoi(dup) != 0;
         std::string str(s);
         size_t pos = 0;
         while (pos <= str.size()) {
             size_t e = str.find(',', pos);
             if (e == std::string::npos) e = str.size();
             if (e > pos) {
-                int v = atoi(str.substr(pos, e - pos).c_str());
-                if (v >= 0 && v < count) d.push_back(v);
+                const std::string tok = str.substr(pos, e - pos);
+                char* end = nullptr;
+                const long v = strtol(tok.c_str(), &end, 10);
+                if (!end || *end || v < 0 || v >= count) {
+                    set_error("MH_DEVICES: '" + tok + "' is not a device id (this process sees " +
+                              std::to_string(count) + " devices)");
+                    return false;
+                }
+                if (!allow_dup && std::find(d.begin(), d.end(), (int)v) != d.end()) {
+                    set_error("MH_DEVICES: device " + tok + " is listed twice");
+                    return false;
+                }
+                d.push_back((int)v);
             }
             pos = e + 1;
         }
     }
-    if (d.empty()) d.push_back(current);
-    return d;
+    if (d.empty()) {
+        set_error("MH_DEVICES names no device");
+        return false;
+    }
+    return true;
 }
 
 // One device's share of a KernelWrapper call, run on its own host thread.
@@ -654,7 +697,8 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
     const int64_t chains = gpuCfg->gridxDim;
     const int iterations = gpuCfg->iterations;
     const size_t n = (size_t)srf->nObjs;
-    std::vector<int> devs = devices_from_env(current);
+    std::vector<int> devs;
+    if (!devices_from_env(current, devs)) return nullptr;
     if ((int64_t)devs.size() > chains) devs.resize((size_t)chains);
 
     point* pts = (point*)malloc(sizeof(point) * n * (size_t)chains);
@@ -682,6 +726,10 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         shards[k].begin = K * (groups * (int64_t)k / (int64_t)devs.size());
         shards[k].count = K * (groups * (int64_t)(k + 1) / (int64_t)devs.size()) - shards[k].begin;
     }
+    // The result buffers are page-locked once, here, for all shards (a shard's slice shares its
+    // boundary pages with its neighbours'); if they cannot be, every shard copies staged.
+    const bool locked_pts = lock_host(pts, sizeof(point) * n * (size_t)chains);
+    const bool locked_costs = lock_host(costs.data(), sizeof(resultCosts) * (size_t)chains);
     auto work = [&](Shard& sh) {
         mh_session* s = session_create(room, sh.device, sh.count, sh.begin, opts);
         if (!s) {
@@ -689,7 +737,7 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
             return;
         }
         sh.ok = session_run(s, iterations, s->stream) && session_finalize(s, s->stream) &&
-                session_download(s, pts + n * sh.begin, costs.data() + sh.begin);
+                session_download(s, pts + n * sh.begin, costs.data() + sh.begin, true);
         if (!sh.ok) sh.err = g_last_error;
         free_session(s);
     };
@@ -701,6 +749,8 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         for (auto& t : th) t.join();
     }
     (void)hipSetDevice(current);
+    if (locked_pts) (void)hipHostUnregister(pts);
+    if (locked_costs) (void)hipHostUnregister(costs.data());
     for (auto& sh : shards) {
         if (!sh.ok) {
             free(pts);
@@ -955,6 +1005,26 @@ MH_API int mh_debug_rng_ex(int rng, uint64_t seed, uint64_t subsequence, int n,
     (void)hipFree(d_n);
     if (e != hipSuccess) {
         set_error(std::string("mh_debug_rng: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+MH_API int mh_debug_math(int fn, uint64_t start, uint64_t count, double* out) {
+    if (fn < 0 || fn >= MH_PROBE_COUNT || !out || count > (1ull << 28)) {
+        set_error("bad arguments");
+        return -1;
+    }
+    if (count == 0) return 0;
+    const size_t bytes = sizeof(double) * (size_t)mh_probe_width(fn) * (size_t)count;
+    double* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d, bytes);
+    if (e == hipSuccess) e = mh::launch_math(fn, start, count, d, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) {
+        set_error(std::string("mh_debug_math: ") + hipGetErrorString(e));
         return -1;
     }
     return 0;

@@ -96,11 +96,9 @@ __device__ __forceinline__ double pose_ry_var(const OwnPose<NPL>& op, int j, int
     double out = 0.0;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
-        const int2 w = *reinterpret_cast<const int2*>(&op.ry[m]);
-        int2 o;
-        o.x = __builtin_amdgcn_ds_bpermute(addr, w.x);
-        o.y = __builtin_amdgcn_ds_bpermute(addr, w.y);
-        out = (m == slot) ? *reinterpret_cast<double*>(&o) : out;
+        const double o = __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(op.ry[m])),
+                                          __builtin_amdgcn_ds_bpermute(addr, __double2loint(op.ry[m])));
+        out = (m == slot) ? o : out;
     }
     return out;
 }
@@ -207,8 +205,8 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     float ti = 0.0f;
     if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
     double a1 = 0.0, a2 = 0.0;
-    if (rel || obj) a1 = atan2(dy, dx);
-    if (rel && obj) a2 = atan2(fy, fx);
+    if (rel || obj) a1 = mh_atan2(dy, dx);
+    if (rel && obj) a2 = mh_atan2(fy, fx);
     if (obj) {
         const float at = (float)(rel ? a2 : a1);
         const float b = at - p.rotYf;
@@ -640,11 +638,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const float prx = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rxs[0])));
             const float pry = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rys[0])));
             const float prr = __int_as_float(__builtin_amdgcn_ds_bpermute(ai, __float_as_int(rrs[0])));
-            const int2 w = *reinterpret_cast<const int2*>(&op.ry[0]);
-            int2 o;
-            o.x = __builtin_amdgcn_ds_bpermute(aj, w.x);
-            o.y = __builtin_amdgcn_ds_bpermute(aj, w.y);
-            const double ryj = *reinterpret_cast<const double*>(&o);
+            const double ryj = __hiloint2double(__builtin_amdgcn_ds_bpermute(aj, __double2hiint(op.ry[0])),
+                                                __builtin_amdgcn_ds_bpermute(aj, __double2loint(op.ry[0])));
             const ObjP q = ch.P[pj];
             float v = 0.0f;
             if (pi < n && pj < n)
@@ -1943,6 +1938,20 @@ __global__ void mh_rng_kernel(uint64_t seed, uint64_t subsequence, int n, unsign
     for (int i = 0; i < n; ++i) nrm[i] = r.normal();
 }
 
+// ---- numerics diagnostic: the shared transcendentals (mh_math.h) on the probe arguments ------
+
+__global__ void __launch_bounds__(256) mh_math_kernel(int fn, uint64_t start, uint64_t count,
+                                                     double* out) {
+    const int w = mh_probe_width(fn);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += stride) {
+        double r[2];
+        mh_math_probe(fn, start + k, r);
+        out[k * w] = r[0];
+        if (w == 2) out[k * w + 1] = r[1];
+    }
+}
+
 // ---- cuRAND XORWOW seeding: curand_init(seed + id, id, 0) per chain (Kernel.cu:159) --------
 
 // rocRAND's xorwow_engine implements the same recurrence and the same 2^67-draw subsequence
@@ -2025,7 +2034,7 @@ __global__ void __launch_bounds__(256) mh_exchange_kernel(LaunchArgs a, int* per
         rocrand_init(a.seed, (1ull << 63) | gid, (uint64_t)(round - 1) * K + k, &st);
         const float u = rocrand_device::detail::uniform_distribution(rocrand(&st));
         const double db = a.ladder[k] - a.ladder[k + 1];
-        const float thr = fminf(1.0f, (float)exp(db * ((double)eb - (double)ea)));
+        const float thr = fminf(1.0f, (float)mh_exp(db * ((double)eb - (double)ea)));
         if (u < thr) {
             pg[k] = cb;
             pg[k + 1] = ca;
@@ -2221,6 +2230,13 @@ hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsi
         hipLaunchKernelGGL(mh_rng_xw_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
     else
         hipLaunchKernelGGL(mh_rng_kernel, dim3(1), dim3(64), 0, s, seed, subsequence, n, u32, uni, nrm);
+    return hipGetLastError();
+}
+
+hipError_t launch_math(int fn, uint64_t start, uint64_t count, double* out, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t blocks = (count + 255) / 256 < 65536 ? (count + 255) / 256 : 65536;
+    hipLaunchKernelGGL(mh_math_kernel, dim3((unsigned)blocks), dim3(256), 0, s, fn, start, count, out);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "mh_launch.h"
+#include "mh_math.h"
 
 #ifndef MH_ABLATE
 #define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
@@ -88,34 +89,32 @@ __device__ __forceinline__ float grp_get(float v, int src, int gbase) {
 
 template <int L>
 __device__ __forceinline__ double grp_get(double v, int src, int gbase) {
-    int2 w = *reinterpret_cast<int2*>(&v);
-    int2 o;
+    const int lo = __double2loint(v), hi = __double2hiint(v);
     if constexpr (L == 64) {
-        o.x = __builtin_amdgcn_readlane(w.x, src);
-        o.y = __builtin_amdgcn_readlane(w.y, src);
+        return __hiloint2double(__builtin_amdgcn_readlane(hi, src),
+                                __builtin_amdgcn_readlane(lo, src));
     } else {
-        o.x = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.x);
-        o.y = __builtin_amdgcn_ds_bpermute((gbase + src) << 2, w.y);
+        return __hiloint2double(__builtin_amdgcn_ds_bpermute((gbase + src) << 2, hi),
+                                __builtin_amdgcn_ds_bpermute((gbase + src) << 2, lo));
     }
-    return *reinterpret_cast<double*>(&o);
 }
 
 // ---- RNG ----------------------------------------------------------------------------------
 
-// Box-Muller in double, rounded to float: (sine branch, cosine branch). Out of line so its
-// OCML log/sin/cos code is not duplicated at every call site.
+// Box-Muller in double, rounded to float: (sine branch, cosine branch). log and sincos are the
+// project's own (mh_math.h), bit-identical to the oracle's by construction.
 __device__ __forceinline__ float2 box_muller_inl(unsigned int a, unsigned int b) {
     if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
     const double u1 = (double)a * 0x1p-32 + 0x1p-33;
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
-    const double rad = sqrt(-2.0 * log(u1));
+    const double rad = sqrt(-2.0 * mh_log(u1));
     const double ang = 6.283185307179586 * u2;
     double s, c;
-    sincos(ang, &s, &c);  // OCML's sin and cos share one argument reduction
+    mh_sincos_medium(ang, &s, &c);  // (one argument reduction for both; ang < 2 pi)
     return make_float2((float)(rad * s), (float)(rad * c));
 }
 
-// Out of line so its OCML log/sin/cos code is not duplicated at every call site.
+// Out of line so its log / sincos code is not duplicated at every call site.
 static __device__ __attribute__((noinline)) float2 box_muller(unsigned int a, unsigned int b) {
     return box_muller_inl(a, b);
 }
@@ -170,18 +169,18 @@ struct ChainRng {
 // cuRAND's Box-Muller for curandStateXORWOW (curand_normal -> _curand_box_muller): float
 // arithmetic on u = x * 2^-32 + 2^-33 and v = y * (2^-32 * 2pi_f) + half of that (one fma, as
 // nvcc contracts it by default), s = sqrtf(-2 logf(u)), (sin(v) * s, cos(v) * s). logf, sinf
-// and cosf are the double functions rounded once to float (the correctly rounded values but
-// for ~2^-29 of inputs); NVIDIA's device path uses the approximate __sincosf, so its normals
-// can differ in the last bits (DESIGN.md "RNG modes"). Out of line, like box_muller.
+// and cosf are the double functions (mh_math.h) rounded once to float (the correctly rounded
+// values but for ~2^-29 of inputs); NVIDIA's device path uses the approximate __sincosf, so its
+// normals can differ in the last bits (DESIGN.md "RNG modes"). Out of line, like box_muller.
 static __device__ __attribute__((noinline)) float2 curand_box_muller(unsigned int x, unsigned int y) {
     constexpr float kInv = 0x1p-32f;
     constexpr float kInv2Pi = 0x1p-32f * 6.2831855f;  // CURAND_2POW32_INV_2PI (exact scaling)
     const float u = (float)x * kInv + kInv * 0.5f;
     const float v = __builtin_fmaf((float)y, kInv2Pi, kInv2Pi * 0.5f);
-    const float lg = (float)log((double)u);
+    const float lg = (float)mh_log((double)u);
     const float s = __builtin_sqrtf(-2.0f * lg);
     double sn, cs;
-    sincos((double)v, &sn, &cs);
+    mh_sincos_medium((double)v, &sn, &cs);  // (v <= 2 pi)
     return make_float2((float)sn * s, (float)cs * s);
 }
 
@@ -457,17 +456,16 @@ __device__ __forceinline__ double distance_f(float xi, float yi, float xj, float
 __device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {
     double dx = (double)(float)(xi - xj);
     double dy = (double)(float)(yi - yj);
-    double tp = atan2(dy, dx);
+    double tp = mh_atan2(dy, dx);
     if (tp < 0) tp = kTwoPI + tp;
     double t = tp - (double)ti;
     return (t < 0) ? kTwoPI + t : t;
 }
 
-// The reference's float atan2f / cosf, evaluated as the double function rounded once.
-__device__ __forceinline__ float atan2_f32(float y, float x) {
-    return (float)atan2((double)y, (double)x);
-}
-__device__ __forceinline__ float cos_f32(float x) { return (float)cos((double)x); }
+// The reference's float atan2f / cosf, evaluated as the double function rounded once
+// (mh_math.h, shared with the oracle).
+__device__ __forceinline__ float atan2_f32(float y, float x) { return mh_atan2_f32(y, x); }
+__device__ __forceinline__ float cos_f32(float x) { return mh_cos_f32(x); }
 
 // minValue/maxValue (Kernel.cu:366-401) of a rectangle translated by (tx, ty), as floats.
 __device__ __forceinline__ float4 shape_box(const RectShape& s, float tx, float ty) {
@@ -782,11 +780,7 @@ struct BoundTerms {
 // One butterfly level of a double: v + (its partner's v), both halves moved by bfly<OFF>.
 template <int OFF>
 __device__ __forceinline__ double bfly_add(double v) {
-    const int2 w = *reinterpret_cast<int2*>(&v);
-    int2 o;
-    o.x = bfly<OFF>(w.x);
-    o.y = bfly<OFF>(w.y);
-    return v + *reinterpret_cast<double*>(&o);
+    return v + __hiloint2double(bfly<OFF>(__double2hiint(v)), bfly<OFF>(__double2loint(v)));
 }
 
 // Sum of a double over the 64 lanes of the wavefront, uniform: six butterfly levels, six fp64
@@ -798,10 +792,8 @@ __device__ __forceinline__ double wave_dsum(double v) {
     v = bfly_add<8>(v);
     v = bfly_add<16>(v);
     v = bfly_add<32>(v);
-    int2 w = *reinterpret_cast<int2*>(&v);
-    w.x = __builtin_amdgcn_readfirstlane(w.x);
-    w.y = __builtin_amdgcn_readfirstlane(w.y);
-    return *reinterpret_cast<double*>(&w);
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
 }
 
 // Sum of v over the 64 lanes of the wavefront, uniform (an SGPR): in-row butterflies (DPP
@@ -1128,7 +1120,7 @@ __device__ __forceinline__ int pick_object(Rng& rng, int n, const unsigned char*
 __device__ __forceinline__ float accept_threshold(double x) {
     if (x >= 0.0) return 1.0f;
     if (x < -24.0) return 0.0f;
-    return fminf(1.0f, (float)exp(x));
+    return fminf(1.0f, (float)mh_exp(x));
 }
 
 // Accept's decision with the proposal's exact total `star` and the current total known only as

@@ -64,6 +64,7 @@ hipError_t launch_step_best(const LaunchArgs& a, int L, int npl, int waves_per_w
 hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsigned int* u32,
                       float* uni, float* nrm, hipStream_t s);
 hipError_t launch_exchange(const LaunchArgs& a, int* perm, int round, hipStream_t s);
+hipError_t launch_math(int fn, uint64_t start, uint64_t count, double* out, hipStream_t s);
 hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
                               hipStream_t s);
 

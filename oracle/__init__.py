@@ -13,6 +13,8 @@ import numpy as np
 ORACLE_DIR = Path(__file__).resolve().parent
 LIB_PATH = ORACLE_DIR / "_build" / "liboracle.so"
 SOURCES = [ORACLE_DIR / "mh_oracle.c"]
+# the shared transcendentals (the only product file the oracle includes besides the wire structs)
+MATH_HEADER = ORACLE_DIR.parent / "metropolis-hastings-gpgpu_amd" / "csrc" / "mh_math.h"
 CFLAGS = ["-O2", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
           "-pthread"]
 
@@ -22,7 +24,8 @@ _lib = None
 def build(force: bool = False) -> Path:
     import subprocess
     LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
-    newest = max(p.stat().st_mtime for p in SOURCES + [ORACLE_DIR / "mh_oracle.h"])
+    newest = max(p.stat().st_mtime for p in SOURCES + [ORACLE_DIR / "mh_oracle.h", MATH_HEADER,
+                                                        ORACLE_DIR.parent / "include" / "mh_kernel.h"])
     if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
         cmd = ["gcc", *CFLAGS, *map(str, SOURCES), "-o", str(LIB_PATH), "-lm"]
         subprocess.run(cmd, check=True)
@@ -89,6 +92,12 @@ def load(pkg=None) -> C.CDLL:
     lib.orc_accept.restype = C.c_int
     lib.orc_accept_at.argtypes = [C.c_double, C.c_double, C.c_double, C.c_void_p]
     lib.orc_accept_at.restype = C.c_int
+    lib.orc_math_apply.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    lib.orc_math_apply.restype = C.c_int
+    for name in ("orc_math_eval", "orc_math_eval_libm"):
+        f = getattr(lib, name)
+        f.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p]
+        f.restype = C.c_int
     _lib = lib
     return lib
 
@@ -215,3 +224,38 @@ def rng_streams(seed: int, subsequence: int, n: int, kind: int = PHILOX):
     r = rng_init(seed, subsequence, kind)
     g = np.array([lib.orc_rng_normal(C.byref(r)) for _ in range(n)], dtype=np.float32)
     return u, f, g
+
+
+# mh_math.h's numerics probes (MH_PROBE_*), in order
+PROBES = ["bm_log", "bm_sincos", "cos_f32", "xw_log", "xw_sincos", "atan2_room", "atan2_bits",
+          "atan2f_room", "atan2f_bits", "exp_accept", "exp_any"]
+
+
+def probe_width(fn: int) -> int:
+    return 2 if PROBES[fn] in ("bm_sincos", "xw_sincos") else 1
+
+
+def math_eval(fn: int, start: int, count: int, threads: int = 8, libm: bool = False) -> np.ndarray:
+    """mh_math.h's probe `fn` (or the C library's, libm=True) at argument indices start ..
+    start + count - 1: float64 [count, width]."""
+    lib = load()
+    out = np.empty((count, probe_width(fn)), dtype=np.float64)
+    f = lib.orc_math_eval_libm if libm else lib.orc_math_eval
+    if f(fn, start, count, threads, out.ctypes.data) != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    return out
+
+
+MATH_FUNCTIONS = {"log": 0, "exp": 1, "sin": 2, "cos": 3, "atan2": 4, "sin_medium": 5}
+
+
+def math_apply(name: str, a, b=None) -> np.ndarray:
+    """mh_math.h's `name` on float64 arguments a (and b for atan2(a, b))."""
+    lib = load()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty_like(a)
+    if lib.orc_math_apply(MATH_FUNCTIONS[name], a.ctypes.data, None if b is None else b.ctypes.data,
+                          len(a), out.ctypes.data) != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    return out

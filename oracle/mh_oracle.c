@@ -8,11 +8,15 @@
  *
  * Math library contract (shared with the device; DESIGN.md "Numerics"):
  *   - sqrt/sqrtf/division: IEEE correctly rounded on both sides;
+ *   - every transcendental -- atan2 in theta, cos/sin of focalRot, exp in Accept, log/sin/cos in
+ *     Box-Muller -- is the project's own (metropolis-hastings-gpgpu_amd/csrc/mh_math.h, fdlibm's
+ *     algorithms, within ~1 ulp), compiled here by gcc and on the device by hipcc from the same
+ *     source out of correctly rounded operations only, so both return the same bits by
+ *     construction (tests/test_gpu_math.py checks it exhaustively on the 32-bit domains). The
+ *     oracle includes that header only: it links nothing else of the product;
  *   - the reference's float transcendentals (atan2f in phi, cosf in FocalPointCosts) are taken
  *     as the double function rounded once to float, which is what a correctly rounded float
- *     library returns except in ~2^-29 of cases;
- *   - double transcendentals (atan2 in theta, cos/sin of focalRot, exp in Accept, log/sin/cos in
- *     Box-Muller) come from libm here and from OCML on the device; both are within ~1 ulp.
+ *     library returns except in ~2^-29 of cases.
  *
  * Defined semantics where the reference is ill-defined:
  *   - one proposer per chain and a full state copy each step (the reference races when
@@ -23,6 +27,7 @@
  */
 #define _GNU_SOURCE
 #include "mh_oracle.h"
+#include "../metropolis-hastings-gpgpu_amd/csrc/mh_math.h"
 
 #include <float.h>
 #include <math.h>
@@ -196,9 +201,11 @@ static float xw_normal(orc_rng* r) {
     const float k2pi = 0x1p-32f * 6.2831855f;
     const float u = (float)a * 0x1p-32f + 0x1p-33f;
     const float v = fmaf((float)b, k2pi, k2pi * 0.5f);
-    const float lg = (float)log((double)u);
+    const float lg = (float)mh_log((double)u);
     const float s = sqrtf(-2.0f * lg);
-    const float sn = (float)sin((double)v), cs = (float)cos((double)v);
+    double snd, csd;
+    mh_sincos_medium((double)v, &snd, &csd);  /* (v <= 2 pi) */
+    const float sn = (float)snd, cs = (float)csd;
     r->bm_val = cs * s;
     r->bm_has = 1;
     return sn * s;
@@ -238,11 +245,13 @@ float orc_rng_normal(orc_rng* r) {
     uint32_t b = orc_rng_next(r);
     double u1 = (double)a * 0x1p-32 + 0x1p-33;
     double u2 = (double)b * 0x1p-32 + 0x1p-33;
-    double rad = sqrt(-2.0 * log(u1));
+    double rad = sqrt(-2.0 * mh_log(u1));
     double ang = 6.283185307179586 * u2;
-    r->bm_val = (float)(rad * cos(ang));
+    double sn, cs;
+    mh_sincos_medium(ang, &sn, &cs);  /* (ang < 2 pi) */
+    r->bm_val = (float)(rad * cs);
     r->bm_has = 1;
-    return (float)(rad * sin(ang));
+    return (float)(rad * sn);
 }
 
 /* rocrand_init(seed, subsequence, offset) for Philox4x32-10. */
@@ -279,15 +288,15 @@ static double distance_f(float xi, float yi, float xj, float yj) {
 static double theta_f(float xi, float yi, float xj, float yj, float ti) {
     double dx = (double)(float)(xi - xj);
     double dy = (double)(float)(yi - yj);
-    double tp = atan2(dy, dx);
+    double tp = mh_atan2(dy, dx);
     if (tp < 0) tp = 2 * ORC_PI + tp;
     double t = tp - (double)ti;
     return (t < 0) ? 2 * ORC_PI + t : t;
 }
 
 /* float atan2 / cos as the double function rounded once (see header comment). */
-static float atan2_f32(float y, float x) { return (float)atan2((double)y, (double)x); }
-static float cos_f32(float x) { return (float)cos((double)x); }
+static float atan2_f32(float y, float x) { return mh_atan2_f32(y, x); }
+static float cos_f32(float x) { return mh_cos_f32(x); }
 
 /* Kernel.cu:185-188: atan2 of float differences (float result), minus tj in float, plus
  * PI/2 in double, rounded to float on return. */
@@ -415,8 +424,8 @@ float orc_symmetry(const orc_room* room, const positionAndRotation* cfg) {
     float acc = 0;
     for (int i = 0; i < n; ++i) {
         float best = 0;
-        float ux = (float)cos(s->focalRot);
-        float uy = (float)sin(s->focalRot);
+        float ux = (float)mh_cos(s->focalRot);
+        float uy = (float)mh_sin(s->focalRot);
         double along_f = s->focalX * ux;
         along_f = along_f + s->focalY * uy;
         double along_i = cfg[i].x * ux;
@@ -641,7 +650,7 @@ long long orc_u1_uphill_draws(int reset) {
 /* Kernel.cu:706-713: maximises the total; exp in double, rounded to float. */
 int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
     float u = orc_rng_uniform(r);
-    float a = fminf(1.0f, (float)exp(ORC_BETA * (cost_star - cost_cur)));
+    float a = fminf(1.0f, (float)mh_exp(ORC_BETA * (cost_star - cost_cur)));
     return u < a;
 }
 
@@ -649,7 +658,7 @@ int orc_accept(double cost_star, double cost_cur, orc_rng* r) {
 int orc_accept_at(double cost_star, double cost_cur, double beta, orc_rng* r) {
     float u = orc_rng_uniform(r);
     if (u == 1.0f && cost_star > cost_cur) __atomic_add_fetch(&g_u1_uphill, 1, __ATOMIC_RELAXED);
-    float a = fminf(1.0f, (float)exp(beta * (cost_star - cost_cur)));
+    float a = fminf(1.0f, (float)mh_exp(beta * (cost_star - cost_cur)));
     return u < a;
 }
 
@@ -830,7 +839,7 @@ static void run_group(const chain_job* job, int64_t g, chain_state* st) {
                                     (uint64_t)(round - 1) * K + k);
                 const float u = orc_rng_uniform(&u_r);
                 const double db = job->ladder[k] - job->ladder[k + 1];
-                const float thr = fminf(1.0f, (float)exp(db * ((double)st[cb].cc.totalCosts -
+                const float thr = fminf(1.0f, (float)mh_exp(db * ((double)st[cb].cc.totalCosts -
                                                                (double)st[ca].cc.totalCosts)));
                 if (u < thr) {
                     perm[k] = cb;
@@ -929,4 +938,113 @@ int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       resultCosts* out_costs, int64_t* out_accepted) {
     return run_chains(room, cfg, opts, chain_begin, n_chains, iterations, nthreads, NULL,
                       out_state, out_costs, out_accepted);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Numerics probes (tests/test_gpu_math.py): the shared math functions on the argument streams
+ * of mh_math.h, and the C library's functions on the same arguments for comparison.
+ * ---------------------------------------------------------------------------------------- */
+static void probe_libm(int fn, uint64_t i, double* out) {
+    const uint32_t w = (uint32_t)i;
+    float y, x;
+    switch (fn) {
+        case MH_PROBE_BM_LOG: out[0] = log((double)w * 0x1p-32 + 0x1p-33); break;
+        case MH_PROBE_BM_SINCOS: {
+            const double a = 6.283185307179586 * ((double)w * 0x1p-32 + 0x1p-33);
+            out[0] = sin(a);
+            out[1] = cos(a);
+            break;
+        }
+        case MH_PROBE_COS_F32: {
+            float v;
+            memcpy(&v, &w, 4);
+            out[0] = (double)(float)cos((double)v);
+            break;
+        }
+        case MH_PROBE_XW_LOG:
+            out[0] = (double)(float)log((double)((float)w * 0x1p-32f + 0x1p-32f * 0.5f));
+            break;
+        case MH_PROBE_XW_SINCOS: {
+            const float k = 0x1p-32f * 6.2831855f;
+            const double v = (double)fmaf((float)w, k, k * 0.5f);
+            out[0] = sin(v);
+            out[1] = cos(v);
+            break;
+        }
+        case MH_PROBE_ATAN2_ROOM:
+        case MH_PROBE_ATAN2_BITS:
+            mh_arg_atan2(i, fn == MH_PROBE_ATAN2_BITS, &y, &x);
+            out[0] = atan2((double)y, (double)x);
+            break;
+        case MH_PROBE_ATAN2F_ROOM:
+        case MH_PROBE_ATAN2F_BITS:
+            mh_arg_atan2(i, fn == MH_PROBE_ATAN2F_BITS, &y, &x);
+            out[0] = (double)(float)atan2((double)y, (double)x);
+            break;
+        default: out[0] = exp(mh_arg_exp(i, fn == MH_PROBE_EXP_ANY)); break;
+    }
+}
+
+typedef struct {
+    int fn, libm;
+    uint64_t start, count;
+    double* out;
+} probe_job;
+
+static void* probe_worker(void* arg) {
+    const probe_job* j = (const probe_job*)arg;
+    const int w = mh_probe_width(j->fn);
+    for (uint64_t k = 0; k < j->count; ++k) {
+        if (j->libm) probe_libm(j->fn, j->start + k, j->out + k * w);
+        else mh_math_probe(j->fn, j->start + k, j->out + k * w);
+    }
+    return NULL;
+}
+
+static int probe_run(int fn, int libm, uint64_t start, uint64_t count, int nthreads, double* out) {
+    if (fn < 0 || fn >= MH_PROBE_COUNT || !out) return fail("bad probe %ld", fn);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    probe_job jobs[256];
+    const int w = mh_probe_width(fn);
+    for (int t = 0; t < nthreads; ++t) {
+        const uint64_t b = count * (uint64_t)t / (uint64_t)nthreads;
+        const uint64_t e = count * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        jobs[t].fn = fn;
+        jobs[t].libm = libm;
+        jobs[t].start = start + b;
+        jobs[t].count = e - b;
+        jobs[t].out = out + b * w;
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, probe_worker, &jobs[t]);
+    probe_worker(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    return 0;
+}
+
+int orc_math_eval(int fn, uint64_t start, uint64_t count, int nthreads, double* out) {
+    return probe_run(fn, 0, start, count, nthreads, out);
+}
+
+int orc_math_eval_libm(int fn, uint64_t start, uint64_t count, int nthreads, double* out) {
+    return probe_run(fn, 1, start, count, nthreads, out);
+}
+
+/* mh_math.h's functions on given arguments (tests/test_math.py measures their accuracy):
+ * which = 0 log, 1 exp, 2 sin, 3 cos, 4 atan2(a, b), 5 sin of the medium reduction only. */
+int orc_math_apply(int which, const double* a, const double* b, int64_t n, double* out) {
+    if (which < 0 || which > 5 || !a || !out || (which == 4 && !b)) return fail("bad function %ld", which);
+    for (int64_t i = 0; i < n; ++i) {
+        double sn, cs;
+        switch (which) {
+            case 0: out[i] = mh_log(a[i]); break;
+            case 1: out[i] = mh_exp(a[i]); break;
+            case 2: out[i] = mh_sin(a[i]); break;
+            case 3: out[i] = mh_cos(a[i]); break;
+            case 4: out[i] = mh_atan2(a[i], b[i]); break;
+            default: mh_sincos_medium(a[i], &sn, &cs); out[i] = sn; break;
+        }
+    }
+    return 0;
 }

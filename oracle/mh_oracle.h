@@ -130,6 +130,19 @@ int orc_run_chains_ex(const orc_room* room, const positionAndRotation* cfg,
                       int iterations, int nthreads, positionAndRotation* out_state,
                       resultCosts* out_costs, int64_t* out_accepted);
 
+/* The numerics probes of mh_math.h (MH_PROBE_*): out receives count x width doubles, probe
+ * `fn` at argument indices start .. start + count - 1, on `nthreads` threads -- the values the
+ * device diagnostic mh_debug_math must reproduce bit for bit. */
+int orc_math_eval(int fn, uint64_t start, uint64_t count, int nthreads, double* out);
+
+/* The same probes evaluated with the C library's log / sin / cos / atan2 / exp instead of
+ * mh_math.h (the oracle's math before round 4), to report how far the two libraries differ. */
+int orc_math_eval_libm(int fn, uint64_t start, uint64_t count, int nthreads, double* out);
+
+/* mh_math.h's functions on given arguments: which = 0 log, 1 exp, 2 sin, 3 cos, 4 atan2(a, b),
+ * 5 sin through the medium-range reduction only (|a| <= 2^20 pi/2). */
+int orc_math_apply(int which, const double* a, const double* b, int64_t n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

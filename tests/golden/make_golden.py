@@ -111,8 +111,10 @@ def main():
     out["rooms"] = {f"synthetic{n}": hashlib.sha256(room_bytes(mh.synthetic_room(n))).hexdigest()
                     for n in (1, 8, 64, 256)}
     path = Path(__file__).with_name("golden.json")
-    if path.exists():  # searched fixtures (find_index_n.py) are kept
-        out["index_n"] = json.loads(path.read_text()).get("index_n", [])
+    if path.exists():  # searched fixtures (find_index_n.py, find_u1_accept.py) are kept
+        old = json.loads(path.read_text())
+        out["index_n"] = old.get("index_n", [])
+        out["u1_accept"] = old.get("u1_accept", [])
     path.write_text(json.dumps(out, indent=1) + "\n")
     print("wrote", path)
 

@@ -207,13 +207,21 @@ def test_config4_two_rank_bench_equals_one_session(mh, hiplib, tmp_path):
 
 
 def test_kernelwrapper_mh_devices_sharding(mh, hiplib, monkeypatch):
-    """$MH_DEVICES=0,0: KernelWrapperSeeded shards the call over two host threads and streams
-    (device 0 twice); the result must equal the single-device call bit for bit."""
+    """$MH_DEVICES=0,0 (with $MH_DEVICES_ALLOW_DUPLICATES=1: a repeated id is otherwise an error):
+    KernelWrapperSeeded shards the call over two host threads and streams (device 0 twice); the
+    result must equal the single-device call bit for bit."""
     room = mh.synthetic_room(64)
     chains, steps, seed = 1000, 300, 4711
     monkeypatch.delenv("MH_DEVICES", raising=False)
     p1, c1 = mh.kernel_wrapper(room, chains, steps, seed=seed)
     monkeypatch.setenv("MH_DEVICES", "0,0")
+    with pytest.raises(mh.MHError, match="listed twice"):  # (not a multi-GPU run)
+        mh.kernel_wrapper(room, 8, 1, seed=seed)
+    monkeypatch.setenv("MH_DEVICES", "0,999")
+    with pytest.raises(mh.MHError, match="not a device id"):
+        mh.kernel_wrapper(room, 8, 1, seed=seed)
+    monkeypatch.setenv("MH_DEVICES", "0,0")
+    monkeypatch.setenv("MH_DEVICES_ALLOW_DUPLICATES", "1")
     p2, c2 = mh.kernel_wrapper(room, chains, steps, seed=seed)
     assert np.array_equal(p1.view(np.uint32), p2.view(np.uint32))
     assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))

@@ -373,7 +373,7 @@ def test_best_of_chain_matches_oracle(mh, orc, hiplib, monkeypatch, step, track,
     room = _room(mh, kind, n)
     seed = 9100 + n + track
     with mh.Session(room, chains, seed=seed, track=track) as s:
-        assert s.step_kernel()[2].split("-")[0] == kind_
+        assert s.step_kernel()[2] == kind_  # (never the few-chains instance)
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -478,7 +478,7 @@ def test_xorwow_chains_match_oracle(mh, orc, hiplib, monkeypatch, step, kind, n,
     room = _room(mh, kind, n)
     seed = 1760000000 + n
     with mh.Session(room, chains, seed=seed, rng=1) as s:
-        assert s.step_kernel()[2].split("-")[0] == kind_
+        assert s.step_kernel()[2] == kind_  # (never the few-chains instance)
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
@@ -551,7 +551,7 @@ def test_tempering_matches_oracle(mh, orc, hiplib, monkeypatch, step, kind, n, K
     room = _room(mh, kind, n)
     seed = 3100 + n + K
     with mh.Session(room, chains, seed=seed, temps=K, swap_interval=interval, beta_min=0.2) as s:
-        assert s.step_kernel()[2].split("-")[0] == kind_
+        assert s.step_kernel()[2] == kind_  # (never the few-chains instance)
         s.run(steps)
         s.finalize()
         pts, costs = s.download()

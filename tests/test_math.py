@@ -1,0 +1,121 @@
+"""The project's transcendentals (metropolis-hastings-gpgpu_amd/csrc/mh_math.h), as the oracle
+compiles them (gcc), measured against 256-bit arithmetic (mpmath) -- their accuracy -- and against
+the C library they replaced in the oracle. The device compiles the same source; its bit identity
+with this build is tests/test_gpu_math.py's subject."""
+import mpmath
+import numpy as np
+import pytest
+
+mpmath.mp.prec = 256
+
+# Error bounds in units in the last place: fdlibm's (log, exp, sin, cos < 1 ulp; atan2 < 2 ulp,
+# the bound CUDA documents for the reference's own atan2).
+ULP_BOUND = {"log": 1.0, "exp": 1.0, "sin": 1.0, "cos": 1.0, "atan2": 2.0, "sin_medium": 1.0}
+EXACT = {"log": mpmath.log, "exp": mpmath.exp, "sin": mpmath.sin, "cos": mpmath.cos,
+         "sin_medium": mpmath.sin, "atan2": mpmath.atan2}
+
+
+def ulp_errors(got, exact_fn, *args):
+    errs = np.empty(len(got))
+    for i in range(len(got)):
+        ex = exact_fn(*[mpmath.mpf(float(a[i])) for a in args])
+        if ex == 0:
+            errs[i] = 0.0 if got[i] == 0 else np.inf
+            continue
+        e = max(int(mpmath.floor(mpmath.log(abs(ex), 2))) - 52, -1074)
+        errs[i] = float(abs(mpmath.mpf(float(got[i])) - ex) / mpmath.mpf(2) ** e)
+    return errs
+
+
+def _args(name, rng, n):
+    if name == "log":
+        return [np.concatenate([rng.random(n // 2) * 0.999 + 2.0 ** -33,  # Box-Muller radii
+                                np.exp(rng.uniform(-700, 700, n // 2)),
+                                2.0 ** rng.uniform(-1074, -1022, 50)])]   # subnormals
+    if name == "exp":
+        return [np.concatenate([rng.uniform(-24, 0, n // 2),  # Accept's thresholds
+                                rng.uniform(-745, 709, n // 2), rng.uniform(-1e-9, 1e-9, 50)])]
+    if name in ("sin", "cos"):
+        return [np.concatenate([rng.uniform(0, 2 * np.pi, n // 2),  # Box-Muller angles
+                                rng.uniform(-1e6, 1e6, n // 4),
+                                rng.uniform(-3e38, 3e38, n // 4).astype(np.float32).astype(np.float64),
+                                2.0 ** rng.uniform(20, 1023, 100) * np.sign(rng.uniform(-1, 1, 100))])]
+    if name == "sin_medium":
+        return [rng.uniform(-1.6e6, 1.6e6, n)]
+    w = rng.uniform(-40, 40, (2, n)).astype(np.float32).astype(np.float64)  # theta's differences
+    return [w[0], w[1]]
+
+
+@pytest.mark.parametrize("name", ["log", "exp", "sin", "cos", "sin_medium", "atan2"])
+def test_accuracy_against_256_bit(orc, name):
+    rng = np.random.default_rng(4)
+    args = _args(name, rng, 3000)
+    got = orc.math_apply(name, *args)
+    err = ulp_errors(got, EXACT[name], *args)
+    assert np.isfinite(err).all()
+    assert err.max() < ULP_BOUND[name], (name, err.max())
+
+
+def test_special_values(orc):
+    inf, nan = np.inf, np.nan
+    log = orc.math_apply("log", [0.0, -0.0, -1.0, inf, nan, 1.0, 2.0 ** -1074])
+    assert log[0] == -inf and log[1] == -inf and np.isnan(log[2]) and log[3] == inf
+    assert np.isnan(log[4]) and log[5] == 0.0
+    assert log[6] == pytest.approx(-744.4400719213812)
+    exp = orc.math_apply("exp", [-inf, inf, nan, 0.0, 710.0, -746.0, -740.0])
+    assert exp[0] == 0.0 and exp[1] == inf and np.isnan(exp[2]) and exp[3] == 1.0
+    assert exp[4] == inf and exp[5] == 0.0 and 0.0 < exp[6] < 1e-320
+    for f in ("sin", "cos"):
+        assert np.isnan(orc.math_apply(f, [inf, -inf, nan])).all()
+    # NaNs are the canonical quiet NaN (x86 and the GPU disagree on an invalid operation's sign)
+    assert (orc.math_apply("cos", [inf]).view(np.uint64) == 0x7FF8000000000000).all()
+    assert orc.math_apply("sin", [0.0])[0] == 0.0 and orc.math_apply("cos", [0.0])[0] == 1.0
+    a = orc.math_apply("atan2", [0.0, -0.0, 0.0, -0.0, 1.0, -1.0, inf, inf, -inf, 1.0, nan],
+                       [1.0, 1.0, -1.0, -1.0, 0.0, 0.0, inf, -inf, inf, -inf, 1.0])
+    assert a[0] == 0.0 and np.signbit(a[1]) and a[2] == np.pi and a[3] == -np.pi
+    assert a[4] == np.pi / 2 and a[5] == -np.pi / 2
+    assert a[6] == np.pi / 4 and a[7] == 3 * np.pi / 4 and a[8] == -np.pi / 4
+    assert a[9] == np.pi and np.isnan(a[10])
+
+
+def test_two_over_pi_table():
+    """mh_math.h's 1280-bit table of 2/pi, re-derived at 1600 bits."""
+    import re
+    from pathlib import Path
+    src = (Path(__file__).resolve().parents[1] / "metropolis-hastings-gpgpu_amd" / "csrc" /
+           "mh_math.h").read_text()
+    body = src[src.index("mh_two_over_pi[40]"):]
+    words = [int(w, 16) for w in re.findall(r"0x([0-9A-F]{8})u", body[:body.index("};")])]
+    assert len(words) == 40
+    with mpmath.workprec(1600):
+        v = int(mpmath.floor(2 / mpmath.pi * mpmath.mpf(2) ** 1280))
+    assert words == [(v >> (32 * (39 - k))) & 0xFFFFFFFF for k in range(40)]
+
+
+def test_medium_reduction_agrees_with_the_general_path(orc):
+    """Box-Muller uses the medium-range reduction alone (its angles lie in (0, 2 pi]); below
+    2^20 pi/2 mh_sincos takes the same path."""
+    x = np.random.default_rng(9).uniform(-1.6e6, 1.6e6, 200000)
+    assert np.array_equal(orc.math_apply("sin_medium", x).view(np.uint64),
+                          orc.math_apply("sin", x).view(np.uint64))
+
+
+@pytest.mark.parametrize("fn", range(11))
+def test_probes_are_deterministic_and_near_libm(orc, fn):
+    """Each probe of the GPU check gives the same bits on any thread count, and differs from the
+    C library (the oracle's math before round 4) only in the last bits: float results in at most
+    2^-20 of the arguments, double results by at most 2 ulp."""
+    a = orc.math_eval(fn, 12345, 1 << 18, threads=8)
+    b = orc.math_eval(fn, 12345, 1 << 18, threads=3)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    g = orc.math_eval(fn, 12345, 1 << 18, threads=8, libm=True)
+    both_nan = np.isnan(a) & np.isnan(g)
+    assert (np.isnan(a) == np.isnan(g)).all()
+    name = orc.PROBES[fn]
+    ok = ~both_nan
+    if name in ("cos_f32", "xw_log", "atan2f_room", "atan2f_bits"):  # float results
+        assert np.mean(a[ok] != g[ok]) <= 2.0 ** -20, name
+    else:
+        d = np.abs(a[ok].view(np.int64) - g[ok].view(np.int64))
+        same_sign = np.sign(a[ok]) == np.sign(g[ok])
+        assert (d[same_sign] <= 2).all(), (name, d.max())

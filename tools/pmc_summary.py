@@ -33,6 +33,11 @@ def load(tag_dir, kernel_substr):
     return {k: sum(v) / len(v) for k, v in per.items()}, meta
 
 
+def _srchash(tag_dir):
+    p = os.path.join(tag_dir, "srchash")
+    return open(p).read().strip() if os.path.exists(p) else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag_dir")
@@ -89,7 +94,10 @@ def main():
                "valu_issue_util": d.get("valu_issue_util"),
                "valu_issue_util_flat": d.get("valu_issue_util_flat"),
                "valu_pricing": "2 cyc/VALU; +2 fp64 add/mul/fma, cvt, f32 trans; +6 f64 trans",
-               "source": os.path.normpath(a.tag_dir), "profile": a.profile}
+               "source": os.path.normpath(a.tag_dir), "profile": a.profile,
+               # the profiled library's source hash (tools/profile_box.sh copied its .srchash):
+               # bench.py uses this record only while the loaded library has the same one
+               "srchash": _srchash(a.tag_dir)}
         with open(a.json, "w") as fh:
             json.dump(rec, fh, indent=1)
         print("wrote", a.json)

@@ -8,6 +8,9 @@ ARGS=${@:---steps 5 --warmup 1 --no-cpu-baseline}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+# the source hash of the library these passes profile (bench.py trusts a PMC record only for it)
+LIB=${MH_LIB:-metropolis-hastings-gpgpu_amd/libmhgpu.so}
+if [ -f "$LIB.srchash" ]; then cp "$LIB.srchash" "$OUT/srchash"; else echo "(no record)" > "$OUT/srchash"; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv \
     -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1 || { echo "kernel-trace pass failed"; exit 1; }
 for PASS in "FETCH_SIZE" "WRITE_SIZE" \
