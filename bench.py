@@ -166,7 +166,7 @@ def pmc_record(n: int, n_chains_per_launch: int, step_kernel: str, srchash: str 
     except Exception as e:  # noqa: BLE001
         return {}, f"unreadable PMC record ({e})"
     k = d.get("kernel", "")
-    kind = ("incremental" if "delta" in k else
+    kind = ("incremental" if "delta" in k else "speculative" if "mh_spec_kernel" in k else
             "full-few" if "mh_kernel<64, 1, 6>" in k else "full")
     if int(d.get("chains_per_launch", -1)) != n_chains_per_launch or kind != step_kernel:
         return {}, "PMC record of another workload"

@@ -262,8 +262,10 @@ MH_API int mh_session_current_costs(mh_session* s, resultCosts* out_costs);
 MH_API int mh_session_summary(mh_session* s, mh_summary* out);
 
 /* Shape of the session's step kernel: lanes per chain, chains per workgroup, and whether it is
- * the incremental-evaluation kernel (1), the full-evaluation kernel (0), or the full-evaluation
- * kernel's instance for launches of few chains (2: no register cap). Any pointer may be NULL. */
+ * the incremental-evaluation kernel (1), the full-evaluation kernel (0), the full-evaluation
+ * kernel's instance for launches of few chains (2: no register cap), or the speculative kernel
+ * (3: rooms of at most 8 objects with few chains; 8 consecutive proposals per wavefront). Any
+ * pointer may be NULL. */
 MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain,
                                int* chains_per_workgroup, int* incremental);
 

@@ -412,11 +412,13 @@ class Session:
 
     def step_kernel(self):
         """(lanes per chain, chains per workgroup, kind) of the step kernel: kind "incremental",
-        "full", or "full-few" (the full-evaluation instance without the register cap, chosen for
-        launches of at most two chains per SIMD)."""
+        "full", "full-few" (the full-evaluation instance without the register cap, chosen for
+        launches of at most two chains per SIMD) or "speculative" (rooms of at most 8 objects
+        with as few chains: mh_spec.hip)."""
         lanes, cpw, inc = C.c_int(), C.c_int(), C.c_int()
         self.lib.mh_session_geometry(self.h, C.byref(lanes), C.byref(cpw), C.byref(inc))
-        return lanes.value, cpw.value, {0: "full", 1: "incremental", 2: "full-few"}[inc.value]
+        return lanes.value, cpw.value, {0: "full", 1: "incremental", 2: "full-few",
+                                        3: "speculative"}[inc.value]
 
     def occupancy(self) -> int:
         """Chains of the step kernel one CU keeps resident (the runtime's occupancy count)."""

@@ -219,6 +219,7 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
 struct Geometry {
     int L, npl, waves;   // full-evaluation kernel (init, final, evaluation; step when !delta)
     bool few;            // step with OP_STEP_FEW (no register cap: too few chains to use it)
+    bool spec;           // step with the speculative kernel (mh_spec.hip)
     mh::ChainLds lay;    // init / step
     int waves_ol;
     mh::ChainLds lay_ol; // final / evaluation (with the OffLimits boxes)
@@ -301,6 +302,13 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
     g.few = plain && g.L == 64 && g.npl <= 1 && n_chains <= 8LL * cus;
     if (const char* e = getenv("MH_STEP_FEW"))
         if (*e) g.few = plain && g.L == 64 && g.npl <= 1 && atoi(e) != 0;
+    // Rooms of at most 8 objects with too few chains to fill the GPU (the few-chains regime):
+    // the speculative kernel evaluates 8 consecutive proposals per wavefront at once and commits
+    // up to the first accepted one. Opt-in ($MH_SPEC=1) while it is slower than OP_STEP_FEW at
+    // config 2 (round 4: 4.39 against 3.92 ms per launch).
+    g.spec = false;
+    if (const char* e = getenv("MH_SPEC"))
+        if (*e) g.spec = plain && mh::spec_fits(n, c, r) && atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
     g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
@@ -524,7 +532,8 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
         if (s->n_temps > 1)  // stop at the next exchange round
             chunk = (int)std::min<int64_t>(chunk, s->swap_interval - s->steps_done % s->swap_interval);
         a.iterations = chunk;
-        if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dwaves, st));
+        if (s->geo.spec) MH_TRY_HIP(mh::launch_spec(a, st));
+        else if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dwaves, st));
         else MH_TRY_HIP(mh::launch(s->geo.few ? mh::OP_STEP_FEW : mh::OP_STEP, a, s->geo.L,
                                    s->geo.npl, s->geo.waves, st));
         done += chunk;
@@ -949,11 +958,11 @@ MH_API int mh_session_summary(mh_session* s, mh_summary* out) {
 MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* chains_per_workgroup,
                                int* incremental) {
     if (!s) { set_error("NULL session"); return -1; }
-    const int L = s->geo.delta ? s->geo.dL : s->geo.L;  // the step kernel's shape
-    const int w = s->geo.delta ? s->geo.dwaves : s->geo.waves;
+    const int L = (s->geo.delta || s->geo.spec) ? 64 : s->geo.L;  // the step kernel's shape
+    const int w = s->geo.spec ? mh::spec_waves() : s->geo.delta ? s->geo.dwaves : s->geo.waves;
     if (lanes_per_chain) *lanes_per_chain = L;
     if (chains_per_workgroup) *chains_per_workgroup = w * (64 / L);
-    if (incremental) *incremental = s->geo.delta ? 1 : (s->geo.few ? 2 : 0);
+    if (incremental) *incremental = s->geo.spec ? 3 : s->geo.delta ? 1 : (s->geo.few ? 2 : 0);
     return 0;
 }
 
@@ -961,7 +970,9 @@ MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
     if (!s || !chains_per_cu) { set_error("NULL argument"); return -1; }
     const auto& g = s->geo;
     int blocks = 0;
-    if (g.delta) {
+    if (g.spec) {
+        *chains_per_cu = mh::spec_blocks_per_cu() * mh::spec_waves();
+    } else if (g.delta) {
         blocks = mh::delta_blocks_per_cu(s->room.rm.n, g.dwaves,
                                          mh::delta_lds_bytes(s->geo.dlay, g.dwaves));
         *chains_per_cu = blocks * g.dwaves;

@@ -205,8 +205,8 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     float ti = 0.0f;
     if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
     double a1 = 0.0, a2 = 0.0;
-    if (rel || obj) a1 = mh_atan2(dy, dx);
-    if (rel && obj) a2 = mh_atan2(fy, fx);
+    if (rel || obj) a1 = atan2_ool(dy, dx);
+    if (rel && obj) a2 = atan2_ool(fy, fx);
     if (obj) {
         const float at = (float)(rel ? a2 : a1);
         const float b = at - p.rotYf;

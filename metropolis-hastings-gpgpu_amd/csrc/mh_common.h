@@ -452,11 +452,39 @@ __device__ __forceinline__ double distance_f(float xi, float yi, float xj, float
     return sqrt(sq);
 }
 
+// The shared transcendentals on the step kernels' rare paths (the exact terms of a step the
+// rejection bound does not decide, Accept's threshold where the bound is open), as value-only
+// helpers (arguments and result in registers). MH_MATH_OOL is a bit mask of the ones compiled
+// out of line (1 atan2, 2 cosf, 4 exp), keeping their code and constants out of the step loop's
+// register allocation; the others are inlined. Which wins is measured per kernel family.
+#ifndef MH_MATH_OOL
+#define MH_MATH_OOL 0  // (A/B, round 4: inlined is faster at configs 3 and 2; mh_delta.hip: 1)
+#endif
+#define MH_OOL_ATTR(bit) __attribute__((MH_OOL_KIND##bit))
+#if MH_MATH_OOL & 1
+#define MH_OOL_KIND1 noinline
+#else
+#define MH_OOL_KIND1 always_inline
+#endif
+#if MH_MATH_OOL & 2
+#define MH_OOL_KIND2 noinline
+#else
+#define MH_OOL_KIND2 always_inline
+#endif
+#if MH_MATH_OOL & 4
+#define MH_OOL_KIND4 noinline
+#else
+#define MH_OOL_KIND4 always_inline
+#endif
+static __device__ MH_OOL_ATTR(1) double atan2_ool(double y, double x) { return mh_atan2(y, x); }
+static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return mh_cos_f32(x); }
+static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return mh_exp(x); }
+
 // Kernel.cu:170-182.
 __device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {
     double dx = (double)(float)(xi - xj);
     double dy = (double)(float)(yi - yj);
-    double tp = mh_atan2(dy, dx);
+    double tp = atan2_ool(dy, dx);
     if (tp < 0) tp = kTwoPI + tp;
     double t = tp - (double)ti;
     return (t < 0) ? kTwoPI + t : t;
@@ -464,8 +492,10 @@ __device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj
 
 // The reference's float atan2f / cosf, evaluated as the double function rounded once
 // (mh_math.h, shared with the oracle).
-__device__ __forceinline__ float atan2_f32(float y, float x) { return mh_atan2_f32(y, x); }
-__device__ __forceinline__ float cos_f32(float x) { return mh_cos_f32(x); }
+__device__ __forceinline__ float atan2_f32(float y, float x) {
+    return (float)atan2_ool((double)y, (double)x);
+}
+__device__ __forceinline__ float cos_f32(float x) { return cos_f32_ool(x); }
 
 // minValue/maxValue (Kernel.cu:366-401) of a rectangle translated by (tx, ty), as floats.
 __device__ __forceinline__ float4 shape_box(const RectShape& s, float tx, float ty) {
@@ -1120,7 +1150,7 @@ __device__ __forceinline__ int pick_object(Rng& rng, int n, const unsigned char*
 __device__ __forceinline__ float accept_threshold(double x) {
     if (x >= 0.0) return 1.0f;
     if (x < -24.0) return 0.0f;
-    return fminf(1.0f, (float)mh_exp(x));
+    return fminf(1.0f, (float)exp_ool(x));
 }
 
 // Accept's decision with the proposal's exact total `star` and the current total known only as

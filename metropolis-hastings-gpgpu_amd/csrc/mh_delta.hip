@@ -27,6 +27,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#ifndef MH_MATH_OOL
+#define MH_MATH_OOL 1  // atan2 out of line in the incremental kernel (config 5: 1% faster)
+#endif
 #include "mh_common.h"
 
 #ifndef MH_STAMPS

@@ -66,19 +66,18 @@ MH_MATH_FN double mh_log(double x) {
                  Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
                  Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
                  Lg7 = 1.479819860511658591e-01;
-    uint64_t u = mh_dbits(x);
-    int32_t hx = (int32_t)(u >> 32);
-    int k = 0;
-    if (hx < 0x00100000) {                       /* x < 2^-1022, zero, negative */
-        if ((u & 0x7FFFFFFFFFFFFFFFull) == 0) return -mh_bitsd(0x7FF0000000000000ull);
-        if (hx < 0) return mh_nan();
-        k = -54;                                 /* subnormal: scale up by 2^54 */
-        x = x * 18014398509481984.0;
-        u = mh_dbits(x);
-        hx = (int32_t)(u >> 32);
+    const uint64_t u0 = mh_dbits(x);
+    const int32_t hx0 = (int32_t)(u0 >> 32);
+    if (hx0 < 0 || hx0 >= 0x7FF00000 || (u0 & 0x7FFFFFFFFFFFFFFFull) == 0) {
+        if ((u0 & 0x7FFFFFFFFFFFFFFFull) == 0) return -mh_bitsd(0x7FF0000000000000ull);
+        if (hx0 < 0) return mh_nan();
+        return (u0 & 0x000FFFFFFFFFFFFFull) || hx0 > 0x7FF00000 ? mh_nan() : x;
     }
-    if (hx >= 0x7FF00000) return (u & 0x000FFFFFFFFFFFFFull) || hx > 0x7FF00000 ? mh_nan() : x;
-    k += (hx >> 20) - 1023;
+    const int sub = hx0 < 0x00100000;            /* subnormal: scale up by 2^54 */
+    x = sub ? x * 18014398509481984.0 : x;
+    const uint64_t u = mh_dbits(x);
+    int32_t hx = (int32_t)(u >> 32);
+    int k = (sub ? -54 : 0) + (hx >> 20) - 1023;
     hx &= 0x000FFFFF;
     const int32_t i = (hx + 0x95F64) & 0x100000;
     /* normalise x or x / 2 into [sqrt(2)/2, sqrt(2)) */
@@ -112,7 +111,7 @@ MH_MATH_FN double mh_exp(double x) {
     const uint64_t u = mh_dbits(x);
     const uint32_t hx = (uint32_t)(u >> 32) & 0x7FFFFFFFu;
     const int xsb = (int)(u >> 63);
-    if (hx >= 0x40862E42u) {                     /* |x| >= 709.78... */
+    if (hx >= 0x40862E42u) {                     /* |x| >= 709.78...: inf, NaN, overflow... */
         if (hx >= 0x7FF00000u) {
             if ((u & 0x000FFFFFFFFFFFFFull) || hx > 0x7FF00000u) return mh_nan();
             return xsb ? 0.0 : x;                /* exp(-inf) = 0, exp(+inf) = inf */
@@ -120,30 +119,24 @@ MH_MATH_FN double mh_exp(double x) {
         if (x > o_threshold) return mh_bitsd(0x7FF0000000000000ull);
         if (x < u_threshold) return 0.0;
     }
-    if (hx < 0x3E300000u) return 1.0 + x;        /* |x| < 2^-28 */
-    double hi = x, lo = 0.0;
-    int k = 0;
-    if (hx > 0x3FD62E42u) {                      /* |x| > ln2 / 2 */
-        if (hx < 0x3FF0A2B2u) {                  /* and |x| < 1.5 ln2 */
-            hi = xsb ? x + ln2HI : x - ln2HI;
-            lo = xsb ? -ln2LO : ln2LO;
-            k = 1 - xsb - xsb;
-        } else {
-            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
-            const double t = (double)k;
-            hi = x - t * ln2HI;                  /* t * ln2HI is exact here */
-            lo = t * ln2LO;
-        }
-        x = hi - lo;
-    }
-    const double t = x * x;
-    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
-    const double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
-    if (k >= -1021) {
-        if (k == 1024) return y * 2.0 * mh_pow2(1023);
-        return y * mh_pow2(k);
-    }
-    return y * mh_pow2(k + 1000) * mh_pow2(-1000);
+    /* the reduction x = k ln2 + (hi - lo): none for |x| <= ln2 / 2, k = +-1 below 1.5 ln2,
+     * k = nearest(x / ln2) above (t * ln2HI is exact there) */
+    const int red = hx > 0x3FD62E42u, near1 = hx < 0x3FF0A2B2u;
+    const int kn = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+    const int k = !red ? 0 : near1 ? 1 - xsb - xsb : kn;
+    const double tk = (double)kn;
+    const double hi = !red ? x : near1 ? (xsb ? x + ln2HI : x - ln2HI) : x - tk * ln2HI;
+    const double lo = !red ? 0.0 : near1 ? (xsb ? -ln2LO : ln2LO) : tk * ln2LO;
+    const double r = red ? hi - lo : x;
+    const double t = r * r;
+    const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    /* y 2^k: in one step for -1021 <= k < 1024, else in two */
+    const double f1 = k == 1024 ? 2.0 : k >= -1021 ? mh_pow2(k < 1023 ? k : 1023)
+                    : mh_pow2(k + 1000 > -1022 ? k + 1000 : -1022);
+    const double f2 = k == 1024 ? mh_pow2(1023) : k >= -1021 ? 1.0 : mh_pow2(-1000);
+    const double e = (y * f1) * f2;
+    return hx < 0x3E300000u ? 1.0 + x : e;       /* |x| < 2^-28 */
 }
 
 /* ---- sin and cos ------------------------------------------------------------------------------ */
@@ -345,7 +338,10 @@ MH_MATH_FN double mh_cos(double x) {
 
 /* ---- atan2 (fdlibm s_atan.c, e_atan2.c) ----------------------------------------------------
  * atan(|t|): the argument reduced to |t'| < 7/16 against atan(0.5), atan(1), atan(1.5) or
- * pi/2 (each in two parts), then t' - t' (s1 + s2), an odd degree-23 minimax polynomial. */
+ * pi/2 (each in two parts), then t' - t' (s1 + s2), an odd degree-23 minimax polynomial.
+ * fdlibm's five-way branch is written as selects of the one division's numerator and
+ * denominator (t' = t / 1 exactly for |t| < 7/16), so a wavefront computes one reduction
+ * whatever mix of ranges its lanes hold; the values are fdlibm's. */
 MH_MATH_FN double mh_atan(double x) {
     const double atanhi0 = 4.63647609000806093515e-01, atanhi1 = 7.85398163397448278999e-01,
                  atanhi2 = 9.82793723247329054082e-01, atanhi3 = 1.57079632679489655800e+00;
@@ -360,93 +356,74 @@ MH_MATH_FN double mh_atan(double x) {
     const uint64_t u = mh_dbits(x);
     const uint32_t ix = (uint32_t)(u >> 32) & 0x7FFFFFFFu;
     const int neg = (int)(u >> 63);
-    if (ix >= 0x44100000u) {                     /* |x| >= 2^66 */
-        if (ix > 0x7FF00000u || (ix == 0x7FF00000u && (u & 0xFFFFFFFFull))) return mh_nan();
-        return neg ? -(atanhi3 + atanlo3) : atanhi3 + atanlo3;
-    }
-    int id = -1;
-    double hi = 0.0, lo = 0.0;
-    if (ix < 0x3FDC0000u) {                      /* |x| < 7/16 */
-        if (ix < 0x3E400000u) return x;          /* |x| < 2^-27 */
-    } else {
-        x = neg ? -x : x;
-        if (ix < 0x3FF30000u) {                  /* |x| < 19/16 */
-            if (ix < 0x3FE60000u) {              /* 7/16 <= |x| < 11/16 */
-                id = 0;
-                x = (2.0 * x - 1.0) / (2.0 + x);
-            } else {                             /* 11/16 <= |x| < 19/16 */
-                id = 1;
-                x = (x - 1.0) / (x + 1.0);
-            }
-        } else if (ix < 0x40038000u) {           /* |x| < 39/16 */
-            id = 2;
-            x = (x - 1.5) / (1.0 + 1.5 * x);
-        } else {                                 /* 39/16 <= |x| < 2^66 */
-            id = 3;
-            x = -1.0 / x;
-        }
-        hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
-        lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
-    }
-    const double z = x * x;
+    if (ix >= 0x7FF00000u && (ix > 0x7FF00000u || (u & 0xFFFFFFFFull))) return mh_nan();
+    const double ax = __builtin_fabs(x);
+    /* id: -1 below 7/16, 0 below 11/16, 1 below 19/16, 2 below 39/16, 3 above */
+    const int id = ix < 0x3FDC0000u ? -1 : ix < 0x3FE60000u ? 0 : ix < 0x3FF30000u ? 1
+                 : ix < 0x40038000u ? 2 : 3;
+    const double num = id < 0 ? x : id == 0 ? 2.0 * ax - 1.0 : id == 1 ? ax - 1.0
+                     : id == 2 ? ax - 1.5 : -1.0;
+    const double den = id < 0 ? 1.0 : id == 0 ? 2.0 + ax : id == 1 ? ax + 1.0
+                     : id == 2 ? 1.0 + 1.5 * ax : ax;
+    const double t = num / den;
+    const double hi = id < 0 ? 0.0 : id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
+    const double lo = id < 0 ? 0.0 : id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+    const double z = t * t;
     const double w = z * z;
     const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
     const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return x - x * (s1 + s2);
-    const double r = hi - ((x * (s1 + s2) - lo) - x);
-    return neg ? -r : r;
+    const double small = t - t * (s1 + s2);               /* |x| < 7/16 (t == x) */
+    const double r = hi - ((t * (s1 + s2) - lo) - t);
+    const double big = neg ? -r : r;
+    return ix < 0x3E400000u ? x                           /* |x| < 2^-27 */
+         : ix >= 0x44100000u ? (neg ? -(atanhi3 + atanlo3) : atanhi3 + atanlo3)  /* >= 2^66 */
+         : id < 0 ? small : big;
 }
 
+/* atan2 (e_atan2.c): the special operands (NaN, zeros, infinities) on a branch of their own;
+ * the general case as selects over atan(|y / x|). (fdlibm's x == 1 shortcut, atan(y), returns
+ * the general case's value -- for |y| > 2^60 both round to pi/2 -- so it is not taken.) */
 MH_MATH_FN double mh_atan2(double y, double x) {
     const double pi_o_4 = 7.8539816339744827900e-01, pi_o_2 = 1.5707963267948965580e+00,
                  pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
     const uint64_t ux = mh_dbits(x), uy = mh_dbits(y);
     const uint32_t ix = (uint32_t)(ux >> 32) & 0x7FFFFFFFu, iy = (uint32_t)(uy >> 32) & 0x7FFFFFFFu;
     const uint32_t lx = (uint32_t)ux, ly = (uint32_t)uy;
-    if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7FF00000u ||
-        (iy | ((ly | (0u - ly)) >> 31)) > 0x7FF00000u)
-        return mh_nan();                         /* x or y is NaN */
     const int m = (int)(uy >> 63) | ((int)(ux >> 63) << 1);  /* 2 sign(x) + sign(y) */
-    if (ux == 0x3FF0000000000000ull) return mh_atan(y);      /* x == 1 */
-    if ((iy | ly) == 0) {                        /* y == 0 */
-        if (m < 2) return y;                     /* atan(+-0, +anything) = +-0 */
-        return m == 2 ? pi : -pi;                /* atan(+-0, -anything) = +-pi */
-    }
-    if ((ix | lx) == 0) return (m & 1) ? -pi_o_2 : pi_o_2;
-    if (ix == 0x7FF00000u) {                     /* x is +-inf */
-        if (iy == 0x7FF00000u) {
+    if (ix >= 0x7FF00000u || iy >= 0x7FF00000u || (ix | lx) == 0 || (iy | ly) == 0) {
+        if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7FF00000u ||
+            (iy | ((ly | (0u - ly)) >> 31)) > 0x7FF00000u)
+            return mh_nan();                     /* x or y is NaN */
+        if ((iy | ly) == 0) {                    /* y == 0 */
+            if (m < 2) return y;                 /* atan(+-0, +anything) = +-0 */
+            return m == 2 ? pi : -pi;            /* atan(+-0, -anything) = +-pi */
+        }
+        if ((ix | lx) == 0) return (m & 1) ? -pi_o_2 : pi_o_2;
+        if (ix == 0x7FF00000u) {                 /* x is +-inf */
+            if (iy == 0x7FF00000u) {
+                switch (m) {
+                    case 0: return pi_o_4;
+                    case 1: return -pi_o_4;
+                    case 2: return 3.0 * pi_o_4;
+                    default: return -3.0 * pi_o_4;
+                }
+            }
             switch (m) {
-                case 0: return pi_o_4;
-                case 1: return -pi_o_4;
-                case 2: return 3.0 * pi_o_4;
-                default: return -3.0 * pi_o_4;
+                case 0: return 0.0;
+                case 1: return -0.0;
+                case 2: return pi;
+                default: return -pi;
             }
         }
-        switch (m) {
-            case 0: return 0.0;
-            case 1: return -0.0;
-            case 2: return pi;
-            default: return -pi;
-        }
+        return (m & 1) ? -pi_o_2 : pi_o_2;       /* y is +-inf */
     }
-    if (iy == 0x7FF00000u) return (m & 1) ? -pi_o_2 : pi_o_2;
     const int k = ((int)iy - (int)ix) >> 20;
-    double z;
-    int mm = m;
-    if (k > 60) {                                /* |y / x| > 2^60 */
-        z = pi_o_2 + 0.5 * pi_lo;
-        mm &= 1;
-    } else if ((ux >> 63) && k < -60) {          /* 0 > |y| / x > -2^-60 */
-        z = 0.0;
-    } else {
-        z = mh_atan(__builtin_fabs(y / x));
-    }
-    switch (mm) {
-        case 0: return z;
-        case 1: return -z;
-        case 2: return pi - (z - pi_lo);
-        default: return (z - pi_lo) - pi;
-    }
+    const int big = k > 60;                                  /* |y / x| > 2^60 */
+    const int tiny = !big && (ux >> 63) && k < -60;          /* 0 > |y| / x > -2^-60 */
+    const double at = mh_atan(__builtin_fabs(y / x));
+    const double z = big ? pi_o_2 + 0.5 * pi_lo : tiny ? 0.0 : at;
+    const int mm = big ? (m & 1) : m;
+    return mm == 0 ? z : mm == 1 ? -z : mm == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
 }
 
 /* ---- the float functions of the reference ----------------------------------------------------

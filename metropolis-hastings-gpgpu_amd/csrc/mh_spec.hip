@@ -1,0 +1,745 @@
+// mh_spec.hip -- the speculative step kernel: rooms of up to 8 objects when the chains are too
+// few to fill the GPU (config 2: N = 8, 1,024 chains, one wavefront per SIMD).
+//
+// A chain's draws do not depend on its accept decisions: the object pick redraws on the static
+// frozen flags only (Kernel.cu:598-602), Box-Muller's cached second normal advances with the
+// draws alone, and Accept draws its uniform on every step (:710). So the proposals of steps
+// t .. t+7 are known before any of them is decided. One chain owns a wavefront; its 64 lanes are
+// K = 8 groups of GL = 8 lanes, and group g holds a copy of the current configuration (lane r:
+// object r) and evaluates proposal t + g against it exactly as the reference does (Costs(),
+// Kernel.cu:516-550, every sum in the reference's order). Steps t .. t+g*-1 before the first
+// accepted proposal g* are rejections, which leave the configuration unchanged, so group g*'s
+// evaluation is exactly the sequential chain's: the batch commits steps t .. t+g* and every
+// group adopts group g*'s configuration; a batch without an acceptance commits all its steps.
+// The result is the sequential chain bit for bit (every decision is Accept's on exact costs);
+// at config 2's ~41% acceptance a batch commits ~2.4 steps for about one step's latency.
+
+#include <stdint.h>
+
+#include "mh_common.h"
+
+#ifndef MH_SPEC_DEBUG
+#define MH_SPEC_DEBUG 0  // diagnostic builds record chain 0's batches (mh_debug_spec); product 0
+#endif
+#if MH_SPEC_DEBUG
+__device__ unsigned int g_spec_dbg[1 << 16];
+__device__ unsigned int g_spec_dbg_n;
+#endif
+#ifndef MH_STAMPS
+#define MH_STAMPS 0  // diagnostic builds: cycles per phase of a batch (tools/stamps.py)
+#endif
+#if MH_STAMPS
+// cycles of the phases of a batch, then batches and committed steps
+__device__ unsigned long long g_spec_cycles[10];
+#define SSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t) :: "memory"); cyc[k] += _t - t_last; t_last = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define SSTAMP(k) do { } while (0)
+#endif
+
+namespace mh {
+namespace {
+
+constexpr int GL = 8;          // lanes per group: the largest room this kernel serves
+constexpr int K = 8;           // groups: proposals evaluated per batch
+constexpr int RMAX = 2 * GL;   // relationship slots (two per lane)
+constexpr int kSpecWaves = 4;  // chains (wavefronts) per workgroup
+
+// Each group's ordered-sum streams (doubles, pre-signed so that every sum is acc + term):
+// VisualBalance area x and area y (Kernel.cu:200-201), FocalPoint -cos(phi) (:277), Symmetry
+// -(row max) (:314), PairWise and PairWiseAngle (:222, :249-253), the non-zero Clearance terms
+// in clearance-major order (:429) and the non-zero SurfaceArea terms (:463-479).
+enum { S_VBX = 0, S_VBY = 8, S_FP = 16, S_SYM = 24, S_PW = 32, S_ANG = 48, S_CL = 64,
+       S_SA = 128, S_END = 192 };
+
+struct SpecRec {  // one step's proposal (the draws of Kernel.cu:576-704, 710)
+    int mode, k1, k2, live;
+    float d1, d2, u, pad;
+};
+
+struct SpecChain {  // LDS of one chain
+    double S[K][S_END];    // each group's ordered-sum streams
+    double SUM[K][8];      // each group's eight sums
+    float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
+    double RY[K][GL];      // each group's double rotY of every object (Symmetry, :305)
+    ObjP P[K][GL];         // each group's float pose words
+    unsigned int wd[128];    // the 128-word window of the Philox stream
+    float bs[128], bc[128];  // Box-Muller pairs (word i, word i + 1) of the window
+};
+
+struct SpecHdr {  // LDS of the workgroup: the room tables
+    RectShape objs[GL];  // off-limits rectangles (pad: area bits)
+    RectShape clrs[GL];  // clearance rectangles (pad: source object)
+    RelConst rel[RMAX];
+};
+
+constexpr int kSpecHdrBytes = (int)((sizeof(SpecHdr) + 15) & ~(size_t)15);
+constexpr int kSpecChainBytes = (int)((sizeof(SpecChain) + 15) & ~(size_t)15);
+
+// A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
+__device__ __attribute__((noinline)) unsigned int philox_far(uint64_t seed, uint64_t sub,
+                                                             uint64_t idx) {
+    return philox_word(seed, sub, idx);
+}
+
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const int a = src << 2;
+    return __hiloint2double(__builtin_amdgcn_ds_bpermute(a, __double2hiint(v)),
+                            __builtin_amdgcn_ds_bpermute(a, __double2loint(v)));
+}
+__device__ __forceinline__ float shfl_f(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ float readlane_f(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+
+// FocalPointCosts term of one object, Kernel.cu:271,277 with phi() of :185-188.
+__device__ __forceinline__ float focal_cos(const DevRoom& rm, float xf, float yf, float ryf) {
+    const float at = atan2_f32(rm.fyf - yf, rm.fxf - xf);
+    const float b = at - ryf;
+    const float ph = (float)((double)b + kHalfPI);
+    return cos_f32(ph);
+}
+
+// PairWise (:210-233) and PairWiseAngle (:236-263) terms of one relationship, exactly.
+__device__ __forceinline__ void rel_exact(const RelConst& rc, const ObjP* P, double& tpw,
+                                          double& tang) {
+    double dy, dx;
+    float ti;
+    tpw = rel_pair(rc, P, dy, dx, ti);
+    tang = rel_angle(rc, mh_atan2(dy, dx), ti);
+}
+
+__device__ __forceinline__ bool touches(const RelConst& rc, int k1, int k2) {
+    auto in = [&](int o) __attribute__((always_inline)) { return o == k1 || o == k2; };
+    return k1 >= 0 && (in(rc.s) || in(rc.t) || in(rc.as) || in(rc.at));
+}
+
+// Row maximum of Symmetry (Kernel.cu:301-312, floored at 0) for the reflected pose (rx, ry, rr)
+// over the n objects of a group's view, screened by the fp32 estimate (mh_common.h sym_val_fast,
+// whose error sym_err bounds): the leader alone is evaluated exactly when it is clear of the
+// runner-up, every candidate within the bound otherwise (max is exact, so the result is the
+// reference's bit for bit).
+__device__ __forceinline__ float sym_row(const ObjP* P, const double* RY, int n, float rx,
+                                         float ry, float rr, bool exact_mode) {
+    float m1 = -INFINITY, m2 = -INFINITY;
+    int j1 = -1;
+    for (int j = 0; j < n; ++j) {
+        const float4 q = *reinterpret_cast<const float4*>(&P[j]);
+        const float v = sym_val_fast(q, rx, ry, rr);
+        m2 = __builtin_amdgcn_fmed3f(m1, m2, v);
+        const bool up = v > m1;
+        m1 = up ? v : m1;
+        j1 = up ? j : j1;
+    }
+    const bool clear = j1 >= 0 && (m2 == -INFINITY || m1 - m2 > sym_err(m1, rr) + sym_err(m2, rr));
+    float best = 0.0f;
+    if (clear && !exact_mode) {
+        const ObjP q = P[j1];
+        best = fmaxf(0.0f, sym_val_exact(q.xf, q.yf, RY[j1], rx, ry, (double)rr));
+    } else {
+        const float thr = (exact_mode || j1 < 0) ? INFINITY : 2.0f * sym_err(fabsf(m1) + 1.0f, rr);
+        for (int j = 0; j < n; ++j) {
+            const ObjP q = P[j];
+            const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rx, ry, rr);
+            if (!(v < m1 - thr)) best = fmaxf(best, sym_val_exact(q.xf, q.yf, RY[j], rx, ry, (double)rr));
+        }
+    }
+    return best;
+}
+
+// Appends the non-zero components of t (when `on`), in lane order within each group, to the
+// group's stream at `pos` (pre-negated: the reference subtracts them); advances pos by the
+// group's count.
+__device__ __forceinline__ void append4(double* S, int& pos, float4 t, bool on, int r) {
+    const int cnt = on ? (int)(t.x != 0.0f) + (int)(t.y != 0.0f) + (int)(t.z != 0.0f) +
+                             (int)(t.w != 0.0f)
+                       : 0;
+    int tot;
+    int q = pos + group_excl_scan<GL>(cnt, r, tot);
+    if (on) {
+        if (t.x != 0.0f) S[q++] = -(double)t.x;
+        if (t.y != 0.0f) S[q++] = -(double)t.y;
+        if (t.z != 0.0f) S[q++] = -(double)t.z;
+        if (t.w != 0.0f) S[q++] = -(double)t.w;
+    }
+    pos += tot;
+}
+
+__global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = __lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 3, r = lane & 7, gbase = lane & ~7;
+    const DevRoom& rm = a.rm;
+    const int n = rm.n, c = rm.c, nr = rm.r;
+
+    SpecHdr* H = reinterpret_cast<SpecHdr*>(lds);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        RectShape s = a.objc[i].off;
+        s.pad = __float_as_int(a.objc[i].area);
+        H->objs[i] = s;
+    }
+    for (int i = threadIdx.x; i < c; i += blockDim.x) {
+        RectShape s = a.clrc[i].shape;
+        s.pad = a.clrc[i].src;
+        H->clrs[i] = s;
+    }
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) H->rel[i] = a.relc[i];
+    __syncthreads();
+
+    const int64_t chain = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (chain >= a.n_chains) return;
+    SpecChain* X = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes + wave * kSpecChainBytes);
+
+    // Frozen flags as a mask, index n frozen (a pick of n is redrawn).
+    unsigned int fz = 1u << n;
+    for (int i = 0; i < n; ++i) fz |= (a.objc[i].frozen != 0 ? 1u : 0u) << i;
+
+    // The current configuration, in every group: lane r holds object r.
+    double* st = a.st + chain * (int64_t)(F_COUNT * n);
+    double cx = 0.0, cy = 0.0, cry = 0.0;
+    if (r < n) {
+        cx = st[F_X * n + r];
+        cy = st[F_Y * n + r];
+        cry = st[F_RY * n + r];
+    }
+    const ChainMeta m0 = a.meta[chain];
+    float cur[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = m0.costs[k];
+
+    // The current configuration's per-object and per-relationship terms (carried across
+    // steps; a proposal recomputes the ones it changes).
+    if (r < n) {
+        ObjP p;
+        p.xf = (float)cx;
+        p.yf = (float)cy;
+        p.rotYf = (float)cry;
+        p.pad = 0.0f;
+        X->P[g][r] = p;
+        X->RY[g][r] = cry;
+    }
+    wave_sync();
+    float cph = 0.0f;
+    double rpw0 = 0.0, rang0 = 0.0, rpw1 = 0.0, rang1 = 0.0;
+    if (r < n) cph = focal_cos(rm, (float)cx, (float)cy, (float)cry);
+    if (r < nr) rel_exact(H->rel[r], X->P[g], rpw0, rang0);
+    if (r + GL < nr) rel_exact(H->rel[r + GL], X->P[g], rpw1, rang1);
+
+    // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i holds
+    // words start + i and start + 64 + i; LDS the words and the Box-Muller pairs of both.
+    const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
+    uint64_t wbase = 0;
+    auto fill = [&](uint64_t at) __attribute__((always_inline)) {
+        wbase = at;
+        const unsigned int w0 = philox_word(seed, sub, at + (uint64_t)lane);
+        const unsigned int w1 = philox_word(seed, sub, at + 64 + (uint64_t)lane);
+        // (both shuffles with every lane active, then the select: a shuffle under `lane < 63`
+        // would read lane 63 while it is inactive, and an inactive source lane reads as 0)
+        const unsigned int d0 = (unsigned int)__shfl_down((int)w0, 1);
+        const unsigned int l0 = (unsigned int)__builtin_amdgcn_readlane((int)w1, 0);
+        const unsigned int n0 = lane < 63 ? d0 : l0;
+        const unsigned int n1 = (unsigned int)__shfl_down((int)w1, 1);  // (lane 63's unused)
+        const float2 z0 = box_muller_inl(w0, n0);
+        const float2 z1 = box_muller_inl(w1, n1);
+        wave_sync();  // (every lane's reads of the previous window are done)
+        X->wd[lane] = w0;
+        X->wd[64 + lane] = w1;
+        X->bs[lane] = z0.x;
+        X->bc[lane] = z0.y;
+        X->bs[64 + lane] = z1.x;
+        X->bc[64 + lane] = z1.y;
+        wave_sync();
+    };
+    fill(m0.draws);
+    unsigned int off = 0;  // next draw - window start (wave-uniform)
+    int bmh = m0.bm_has;
+    float bmv = m0.bm_val;
+    // Draws at a lane's own offset (every lane may read a different one).
+    auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
+        return o < 128 ? X->wd[o] : philox_far(seed, sub, wbase + o);
+    };
+    auto uni_v = [&](unsigned int& o) __attribute__((always_inline)) {
+        return rocrand_device::detail::uniform_distribution(word_v(o++));
+    };
+    auto rand_v = [&](unsigned int& o, int mx) __attribute__((always_inline)) {  // generateRandomIntInRange, Kernel.cu:566-574
+        float u = uni_v(o);
+        u = (float)((double)u * ((double)mx + 0.999999));
+        u = u + 0.0f;
+        return (int)truncf(u);
+    };
+    auto rand_w = [&](unsigned int w, int mx) __attribute__((always_inline)) {  // the same, of a word already read
+        float u = rocrand_device::detail::uniform_distribution(w);
+        u = (float)((double)u * ((double)mx + 0.999999));
+        u = u + 0.0f;
+        return (int)truncf(u);
+    };
+    auto pick_v = [&](unsigned int& o) __attribute__((always_inline)) {  // Kernel.cu:598-602 (index n counts as frozen)
+        int k = rand_v(o, n - 1);
+        while ((fz >> k) & 1u) k = rand_v(o, n - 1);
+        return k;
+    };
+    // The Box-Muller pair (word p, word p + 1): the window's table, or computed past it.
+    auto pair_v = [&](unsigned int p) __attribute__((always_inline)) -> float2 {
+        if (p < 127) return make_float2(X->bs[p], X->bc[p]);
+        return box_muller_inl(word_v(p), word_v(p + 1));
+    };
+
+    unsigned int accepted = 0;
+    const float rx_sx = rm.sx, rx_sy = rm.sy;
+#if MH_STAMPS
+    unsigned long long cyc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
+#endif
+#pragma clang loop unroll(disable)
+    for (int done = 0; done < a.iterations;) {
+        int kb = min(K, a.iterations - done);
+        // At most ~5 draws per step (more only for frozen-object redraws, which then draw past
+        // the window directly): refill unless 48 remain.
+        if (off > 128 - 48) {
+            fill(wbase + off);
+            off = 0;
+        }
+        SSTAMP(0);
+        // Where each step of the batch starts in the stream. A step's draws (Kernel.cu:576-710):
+        // the mode, the picks (with frozen redraws), the normals, Accept's uniform. Only the
+        // normals depend on the state before the step (a cached second normal, h): translate
+        // takes one pair either way (h unchanged, the pair's second normal cached when h = 1),
+        // rotate one pair when h = 0 (then cached) and none when h = 1, swap none. So lane i
+        // parses the mode and picks of a step starting at off + i, and a wave-uniform walk of
+        // at most 8 hops chains the batch's steps; a step starting past off + 63 (or past word
+        // 123) ends the batch early.
+        int pmode = 3, pk1 = -1, pk2 = -1, pafter = 0;  // (3: not parsed, the walk stops there)
+        {
+            const unsigned int o0 = off + (unsigned int)lane;
+            if (o0 < 124) {
+                const unsigned int wa = X->wd[o0], wb = X->wd[o0 + 1], wc = X->wd[o0 + 2];
+                unsigned int o = o0 + 1;
+                pmode = rand_w(wa, 2);
+                if (pmode != 2 || n >= 2) {
+                    pk1 = rand_w(wb, n - 1);
+                    o = o0 + 2;
+                    while ((fz >> pk1) & 1u) pk1 = rand_v(o, n - 1);
+                    if (pmode == 2) {
+                        pk2 = rand_w(o == o0 + 2 ? wc : word_v(o), n - 1);
+                        ++o;
+                        while ((fz >> pk2) & 1u) pk2 = rand_v(o, n - 1);
+                    }
+                }
+                pafter = (int)o;
+            }
+        }
+        // The walk: state (o, h, cache position: -1 = the batch's incoming cached normal).
+        unsigned int go = off, gnext = off + 1;  // lanes of group s: step s's start and the next's
+        int gh = 0, gcp = -1;            // and step s's cache flag and position
+        unsigned int wo = off;
+        int wh = bmh, wcp = -1;
+        for (int s = 0; s < kb; ++s) {
+            const int i = (int)(wo - off);
+            const int md = i < 64 ? __builtin_amdgcn_readlane(pmode, i) : 3;
+            if (md == 3) {
+                kb = s;
+                break;
+            }
+            go = g == s ? wo : go;
+            gh = g == s ? wh : gh;
+            gcp = g == s ? wcp : gcp;
+            const unsigned int pa = (unsigned int)__builtin_amdgcn_readlane(pafter, i);
+            if (md == 0) {  // translate
+                if (wh) wcp = (int)pa;
+                wo = pa + 3;
+            } else if (md == 1) {  // rotate
+                if (!wh) {
+                    wcp = (int)pa;
+                    wo = pa + 3;
+                } else {
+                    wo = pa + 1;
+                }
+                wh = !wh;
+            } else {  // swap
+                wo = pa + 1;
+            }
+            gnext = g == s ? wo : gnext;
+        }
+        // Group g's step from lane (start - off)'s parse, its normals and Accept's uniform.
+        SpecRec R;
+        R.live = g < kb;
+        float bv_out;  // the cached second normal after the step (when h_out)
+        int h_out;
+        {
+            const int src = (int)(go - off) << 2;
+            R.mode = __builtin_amdgcn_ds_bpermute(src, pmode);
+            R.k1 = __builtin_amdgcn_ds_bpermute(src, pk1);
+            R.k2 = __builtin_amdgcn_ds_bpermute(src, pk2);
+            const unsigned int pa = (unsigned int)__builtin_amdgcn_ds_bpermute(src, pafter);
+            const float2 z = make_float2(X->bs[pa < 127 ? pa : 0], X->bc[pa < 127 ? pa : 0]);
+            const float bv = gcp < 0 ? bmv : X->bc[gcp < 127 ? gcp : 0];
+            const unsigned int wu = word_v(gnext - 1);
+            float zs = z.x, zc = z.y, bvi = bv;
+            if (__builtin_expect(pa >= 127 || gcp >= 127, 0)) {  // pairs past the table
+                if (pa >= 127) {
+                    const float2 zz = pair_v(pa);
+                    zs = zz.x;
+                    zc = zz.y;
+                }
+                if (gcp >= 127) bvi = pair_v((unsigned int)gcp).y;
+            }
+            R.d1 = 0.0f;
+            R.d2 = 0.0f;
+            h_out = gh;
+            bv_out = bvi;
+            if (R.mode == 0) {  // translate, Kernel.cu:595-632
+                R.d1 = (gh ? bvi : zs) * rx_sx;
+                R.d2 = (gh ? zs : zc) * rx_sy;
+                bv_out = zc;
+            } else if (R.mode == 1) {  // rotate, :634-653
+                const float dr = gh ? bvi : zs;
+                R.d1 = (float)((double)dr * kSigmaT);
+                h_out = !gh;
+                bv_out = gh ? bvi : zc;
+            } else if (n < 2) {  // swap of a single object draws nothing (:657)
+                R.k1 = -1;
+                R.k2 = -1;
+            }
+            R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
+            R.pad = 0.0f;
+        }
+        SSTAMP(1);
+        const bool live = R.live != 0;
+        const int k1 = live ? R.k1 : -1, k2 = live ? R.k2 : -1;
+
+        // Apply group g's proposal to its copy (Kernel.cu:576-704).
+        double sx = cx, sy = cy, sry = cry;
+        bool moved = false;
+        if (live && R.mode == 0 && r == k1) {
+            moved = true;
+            if (sx + (double)R.d1 > rm.rmax_x) sx = rm.rmax_x;
+            else if (sx + (double)R.d1 < rm.rmin_x) sx = rm.rmin_x;
+            else sx = sx + (double)R.d1;
+            if (sy + (double)R.d2 > rm.rmax_y) sy = rm.rmax_y;
+            else if (sy + (double)R.d2 < rm.rmin_y) sy = rm.rmin_y;
+            else sy = sy + (double)R.d2;
+        } else if (live && R.mode == 1 && r == k1) {
+            moved = true;
+            sry = sry + (double)R.d1;
+            if (sry < 0) sry = sry + kTwoPI;
+            else if (sry > kTwoPI) sry = sry - kTwoPI;
+        }
+        if (__ballot(live && R.mode == 2 && k1 >= 0)) {  // (every lane active for the shuffles)
+            const int ia = gbase + (k1 >= 0 ? k1 : 0), ib = gbase + (k2 >= 0 ? k2 : 0);
+            const double ax = shfl_d(cx, ia), ay = shfl_d(cy, ia), ary = shfl_d(cry, ia);
+            const double bx = shfl_d(cx, ib), by = shfl_d(cy, ib), bry = shfl_d(cry, ib);
+            if (live && R.mode == 2 && k1 >= 0) {
+                // object 1 takes object 2's pose, object 2 object 1's through float temporaries
+                if (r == k2) {
+                    sx = (double)(float)ax;
+                    sy = (double)(float)ay;
+                    sry = (double)(float)ary;
+                    moved = true;
+                } else if (r == k1) {
+                    sx = bx;
+                    sy = by;
+                    sry = bry;
+                    moved = true;
+                }
+            }
+        }
+        const float xf = (float)sx, yf = (float)sy, ryf = (float)sry;
+        if (r < n) {
+            ObjP p;
+            p.xf = xf;
+            p.yf = yf;
+            p.rotYf = ryf;
+            p.pad = 0.0f;
+            X->P[g][r] = p;
+            X->RY[g][r] = sry;
+        }
+        wave_sync();
+        SSTAMP(2);
+        const ObjP* Pg = X->P[g];
+
+        // Per-object terms of the proposal's configuration.
+        float cphs = cph;
+        double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
+        const bool t0 = r < nr && touches(H->rel[r], k1, k2);
+        const bool t1 = r + GL < nr && touches(H->rel[r + GL], k1, k2);
+        if (nr + 2 <= GL) {
+            // One atan2 per lane: lane r < nr for relationship r, lanes nr and nr + 1 for the
+            // FocalPoint terms of the moved objects k1 and k2; the cosines go back to them.
+            const int fo = r == nr ? k1 : (r == nr + 1 ? k2 : -1);
+            const bool foc = fo >= 0;
+            const ObjP q = Pg[foc ? fo : 0];
+            double ay = 0.0, ax = 1.0;
+            float ti = 0.0f;
+            if (t0) pw0 = rel_pair(H->rel[r], Pg, ay, ax, ti);
+            if (foc) {
+                ay = (double)(rm.fyf - q.yf);
+                ax = (double)(rm.fxf - q.xf);
+            }
+            float cf = 0.0f;
+            if (__ballot(foc || t0)) {
+                const double at = atan2_ool(ay, ax);
+                if (t0) an0 = rel_angle(H->rel[r], at, ti);
+                if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
+                    const float b = (float)at - q.rotYf;
+                    cf = cos_f32((float)((double)b + kHalfPI));
+                }
+            }
+            const float c1 = shfl_f(cf, gbase + nr), c2 = shfl_f(cf, gbase + nr + 1);
+            if (moved) cphs = r == k2 ? c2 : c1;  // (a swap's k2 branch wins, as in the apply)
+        } else if (__ballot(moved || t0 || t1)) {
+            if (moved) cphs = focal_cos(rm, xf, yf, ryf);
+            if (t0) rel_exact(H->rel[r], Pg, pw0, an0);
+            if (t1) rel_exact(H->rel[r + GL], Pg, pw1, an1);
+        }
+        SSTAMP(3);
+        float4 box = make_float4(0.f, 0.f, 0.f, 0.f), sao = box, sac = box;
+        bool wild = false;
+        float best = 0.0f;
+        if (r < n) {
+            const RectShape os = H->objs[r];
+            const float area = __int_as_float(os.pad);
+            X->S[g][S_VBX + r] = (double)area * sx;  // Kernel.cu:200-201
+            X->S[g][S_VBY + r] = (double)area * sy;
+            X->S[g][S_FP + r] = -(double)cphs;
+            box = shape_box(os, xf, yf);
+            sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
+            wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
+        }
+        if (r < c) {
+            const RectShape cs = H->clrs[r];
+            const ObjP ps = Pg[cs.pad];
+            X->CLB[g][r] = shape_box(cs, ps.xf, ps.yf);     // Clearance, :414-415
+            sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
+        }
+        if (r < nr) {
+            X->S[g][S_PW + r] = -pw0;
+            X->S[g][S_ANG + r] = -an0;
+        }
+        if (r + GL < nr) {
+            X->S[g][S_PW + r + GL] = -pw1;
+            X->S[g][S_ANG + r + GL] = -an1;
+        }
+        // Symmetry row r, Kernel.cu:292-312.
+        const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
+        if (r < n) {
+            double al = sx * (double)rm.ux;
+            al = al + sy * (double)rm.uy;
+            const float sd = (float)(2.0 * (rm.along_f - al));
+            const float rxr = (float)(sx + (double)(sd * rm.ux));
+            const float ryr = (float)(sy + (double)(sd * rm.uy));
+            float rr = (float)(rm.two_focal_rot - sry);
+            if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
+            best = sym_row(Pg, X->RY[g], n, rxr, ryr, rr, exact_mode);
+            X->S[g][S_SYM + r] = -(double)best;
+        }
+        wave_sync();
+        SSTAMP(4);
+        // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
+        // (clearances, then objects, :445-480), compacted in the reference's order.
+        int ncl = 0, nsa = 0;
+        for (int i = 0; i < c; ++i) {
+            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < n) t4.x = overlap(X->CLB[g][i], box);
+            append4(&X->S[g][S_CL], ncl, t4, r < n, r);
+        }
+        append4(&X->S[g][S_SA], nsa, sac, r < c, r);
+        append4(&X->S[g][S_SA], nsa, sao, r < n, r);
+        wave_sync();
+        SSTAMP(5);
+        // The eight ordered sums: lane r of each group replays stream r (float sums round every
+        // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2).
+        {
+            int base = S_VBX, len = n;
+            bool rnd = true;
+            switch (r) {
+                case 0: base = S_VBX; len = n; rnd = true; break;
+                case 1: base = S_VBY; len = n; rnd = true; break;
+                case 2: base = S_FP; len = n; rnd = false; break;
+                case 3: base = S_SYM; len = n; rnd = true; break;
+                case 4: base = S_CL; len = ncl; rnd = true; break;
+                case 5: base = S_SA; len = nsa; rnd = true; break;
+                case 6: base = S_PW; len = nr; rnd = false; break;
+                default: base = S_ANG; len = nr; rnd = false; break;
+            }
+            const double* src = &X->S[g][base];
+            double acc = 0.0;
+            for (int l = 0; l < len; ++l) {
+                const double s = acc + src[l];
+                acc = rnd ? (double)(float)s : s;
+            }
+            X->SUM[g][r] = acc;
+        }
+        wave_sync();
+        SSTAMP(6);
+        // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547).
+        float sc[8];
+        {
+            const double* sm = X->SUM[g];
+            const float nx = (float)sm[0], ny = (float)sm[1];
+            const double fpd = sm[2];
+            const float symf = (float)sm[3], clf = (float)sm[4], saf = (float)sm[5];
+            const float pw = (float)(sm[6] * sm[7]);
+            const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
+            sc[1] = rm.w_pw * pw;
+            sc[2] = rm.w_vb * vb;
+            sc[3] = rm.w_fp * (float)fpd;
+            sc[4] = rm.w_sym * symf;
+            sc[6] = rm.w_ol * 0.0f;
+            sc[5] = rm.w_cl * clf;
+            sc[7] = rm.w_sa * saf;
+            float t = sc[1] + sc[2];
+            t = t + sc[3];
+            t = t + sc[4];
+            t = t + sc[5];
+            t = t + sc[7];
+            sc[0] = t;
+        }
+        // Accept (Kernel.cu:706-713) for every live proposal against the current total; the
+        // first accepted one ends the batch.
+        const bool acc_g = live && R.u < accept_threshold(kBeta * ((double)sc[0] - (double)cur[0]));
+        const uint64_t bal = __ballot(acc_g && r == 0);
+        const int gs = bal ? (int)(__builtin_ctzll(bal) >> 3) : -1;
+        const int committed = gs >= 0 ? gs + 1 : kb;
+        if (gs >= 0) {
+            const int src = (gs << 3) + r;
+            cx = shfl_d(sx, src);
+            cy = shfl_d(sy, src);
+            cry = shfl_d(sry, src);
+            cph = shfl_f(cphs, src);
+            rpw0 = shfl_d(pw0, src);
+            rang0 = shfl_d(an0, src);
+            rpw1 = shfl_d(pw1, src);
+            rang1 = shfl_d(an1, src);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], gs << 3);
+            ++accepted;
+            // An accepted swap also exchanges z, rotX and rotZ (:675-700), object 1's values
+            // through float temporaries; no cost reads them, so they live in HBM only.
+            const int smode = __builtin_amdgcn_readlane(R.mode, gs << 3);
+            const int sk1 = __builtin_amdgcn_readlane(R.k1, gs << 3);
+            const int sk2 = __builtin_amdgcn_readlane(R.k2, gs << 3);
+            if (smode == 2 && sk1 >= 0 && lane == 0) {
+#pragma unroll
+                for (int f = 0; f < 3; ++f) {
+                    double* row = st + (F_Z + f) * n;
+                    const double va = row[sk1], vb = row[sk2];
+                    row[sk1] = vb;
+                    row[sk2] = (double)(float)va;
+                }
+            }
+        }
+#if MH_SPEC_DEBUG
+        if (chain == 0) {  // [done, kb, off, bmh, gs, committed, cur0] then per group 8 words
+            const unsigned int base = g_spec_dbg_n;
+            if (base + 7 + 8 * K < (1u << 16)) {
+                if (lane == 0) {
+                    g_spec_dbg[base + 0] = (unsigned)done;
+                    g_spec_dbg[base + 1] = (unsigned)kb;
+                    g_spec_dbg[base + 2] = off;
+                    g_spec_dbg[base + 3] = (unsigned)bmh;
+                    g_spec_dbg[base + 4] = (unsigned)gs;
+                    g_spec_dbg[base + 5] = (unsigned)committed;
+                    g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
+                }
+                if (r == 0) {
+                    unsigned int* q = g_spec_dbg + base + 7 + 8 * g;
+                    q[0] = (unsigned)R.mode;
+                    q[1] = (unsigned)R.k1;
+                    q[2] = (unsigned)R.k2;
+                    q[3] = (unsigned)R.live;
+                    q[4] = __float_as_uint(R.d1);
+                    q[5] = __float_as_uint(R.d2);
+                    q[6] = __float_as_uint(R.u);
+                    q[7] = __float_as_uint(sc[0]);
+                }
+                if (lane == 0) g_spec_dbg_n = base + 7 + 8 * K;
+            }
+        }
+#endif
+        // The stream's state after the committed steps: what the last of them leaves.
+        off = (unsigned int)__builtin_amdgcn_readlane((int)gnext, (committed - 1) << 3);
+        bmh = __builtin_amdgcn_readlane(h_out, (committed - 1) << 3);
+        bmv = readlane_f(bv_out, (committed - 1) << 3);
+        done += committed;
+        SSTAMP(7);
+#if MH_STAMPS
+        cyc[8] += 1;
+        cyc[9] += (unsigned long long)committed;
+#endif
+    }
+#if MH_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
+#endif
+
+    if (lane < n) {
+        st[F_X * n + r] = cx;
+        st[F_Y * n + r] = cy;
+        st[F_RY * n + r] = cry;
+    }
+    if (lane == 0) {
+        ChainMeta m = m0;
+        m.accepted = m0.accepted + accepted;
+        m.draws = wbase + off;
+        m.bm_has = bmh;
+        m.bm_val = bmv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
+        a.meta[chain] = m;
+    }
+}
+
+}  // namespace
+
+#if MH_SPEC_DEBUG
+extern "C" __attribute__((visibility("default"))) int mh_debug_spec(unsigned int* out, int cap) {
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_spec_dbg_n), sizeof(n)) != hipSuccess) return -1;
+    if ((int)n > cap) n = (unsigned)cap;
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_dbg), sizeof(unsigned) * n) != hipSuccess) return -1;
+    const unsigned int zero = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_spec_dbg_n), &zero, sizeof(zero));
+    return (int)n;
+}
+#endif
+
+#if MH_STAMPS
+extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_cycles), sizeof(unsigned long long) * 10) != hipSuccess)
+        return -1;
+    unsigned long long zero[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_spec_cycles), zero, sizeof(zero));
+    return 0;
+}
+#endif
+
+size_t spec_lds_bytes(int waves_per_wg) {
+    return (size_t)kSpecHdrBytes + (size_t)waves_per_wg * kSpecChainBytes;
+}
+
+int spec_waves() { return kSpecWaves; }
+
+// Whether the speculative kernel serves a room: at most GL objects, RMAX relationships.
+bool spec_fits(int n, int c, int r) { return n >= 1 && n <= GL && c <= GL && r <= RMAX; }
+
+int spec_blocks_per_cu() {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel, 64 * kSpecWaves,
+                                                     spec_lds_bytes(kSpecWaves)) != hipSuccess)
+        return 0;
+    return blocks;
+}
+
+hipError_t launch_spec(const LaunchArgs& a, hipStream_t s) {
+    if (a.n_chains <= 0) return hipSuccess;
+    const int64_t blocks = (a.n_chains + kSpecWaves - 1) / kSpecWaves;
+    hipLaunchKernelGGL(mh_spec_kernel, dim3((unsigned)blocks), dim3(64 * kSpecWaves),
+                       spec_lds_bytes(kSpecWaves), s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mh

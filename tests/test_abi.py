@@ -75,14 +75,17 @@ def _device_functions(lib_path, tmp_path):
 def test_step_kernels_make_no_calls(mh, tmp_path):
     """Every device function that takes references to a kernel's private objects (eval_costs,
     propose, the incremental kernel's helpers) is inlined: an out-of-line call of eval_costs
-    faulted on MI355X (DESIGN.md "The counting-build fault"). Only the value-only Box-Muller
-    helpers may stay out of line."""
+    faulted on MI355X (DESIGN.md "The counting-build fault"). Only value-only helpers may stay
+    out of line: the Box-Muller transforms, the rare-path transcendentals (mh_common.h) and the
+    speculative kernel's Philox words past its window."""
     names, objects = _device_functions(mh.LIB_PATH, tmp_path)
-    assert objects == 4  # mh_chain, mh_chain_xw, mh_chain_best, mh_delta
+    assert objects == 5  # mh_chain, mh_chain_xw, mh_chain_best, mh_delta, mh_spec
     kernels = {n for n in names if "_kernel" in n}
     assert any("mh_kernelILi64ELi1ELi1E" in n for n in kernels)
     helpers = names - kernels
-    allowed = {"_ZN2mhL10box_mullerEjj", "_ZN2mhL17curand_box_mullerEjj"}
+    allowed = {"_ZN2mhL10box_mullerEjj", "_ZN2mhL17curand_box_mullerEjj", "_ZN2mhL9atan2_oolEdd",
+               "_ZN2mhL11cos_f32_oolEf", "_ZN2mhL7exp_oolEd",
+               "_ZN2mh12_GLOBAL__N_110philox_farEmmm"}  # (mh_spec.hip: redraws past the window)
     assert helpers <= allowed, sorted(helpers - allowed)
 
 

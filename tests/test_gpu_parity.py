@@ -53,6 +53,7 @@ def _use_step(monkeypatch, step: str, n: int) -> str:
     Returns the step-kernel kind the session must report."""
     kind = step.split("-")[0]
     monkeypatch.setenv("MH_DELTA", "1" if kind == "incremental" else "0")
+    monkeypatch.setenv("MH_SPEC", "0")  # (tests/test_gpu_spec.py covers the speculative kernel)
     if step == "full-narrow":
         if _narrow_lanes(n) == 64:
             pytest.skip("the narrow instance is the default one for this N")

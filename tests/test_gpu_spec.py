@@ -1,0 +1,94 @@
+"""The speculative step kernel (mh_spec.hip: rooms of at most 8 objects with few chains; each
+wavefront evaluates 8 consecutive proposals of one chain and commits up to the first accepted
+one) against the oracle's sequential chain, bit for bit: every chain's final poses and costs."""
+import numpy as np
+import pytest
+
+from parity_util import check_chains
+
+pytestmark = pytest.mark.gpu
+
+PI = 3.1416
+
+
+def _room(mh, kind, n):
+    if kind == "frozen":
+        return mh.synthetic_room(n, freeze_every=3)
+    if kind == "manyrel":
+        return mh.synthetic_room(n, n_rel=16 if n > 1 else None)
+    room = mh.synthetic_room(n)
+    if kind == "wrap":  # angle ranges crossing zero: the fmodf branch of Kernel.cu:245-250
+        for k in range(room.srf.nRelationships):
+            room.rsa[k].angleMin = 7 * PI / 4
+            room.rsa[k].angleMax = PI / 4
+    if kind == "cramped":  # objects piled up: many Clearance / SurfaceArea terms, symmetry ties
+        for j in range(n):
+            room.cfg[j].x = 0.3 * (j % 3)
+            room.cfg[j].y = 0.2 * (j // 3)
+            room.cfg[j].rotY = 0.0
+    return room
+
+
+@pytest.mark.parametrize("kind,n,chains,steps", [
+    ("syn", 8, 1024, 2000),   # config 2's room and chain count
+    ("syn", 8, 300, 2500),    # three launches: batches end at a launch's last step
+    ("syn", 1, 64, 500),      # a single object: swaps draw nothing (Kernel.cu:657)
+    ("syn", 2, 128, 800),
+    ("syn", 5, 256, 700),
+    ("frozen", 8, 256, 900),  # frozen picks are redrawn
+    ("manyrel", 8, 128, 600),  # 16 relationships: two slots per lane
+    ("wrap", 8, 128, 600),
+    ("cramped", 8, 128, 600),
+    ("frozen", 3, 64, 400),
+])
+def test_spec_chains_match_oracle(mh, orc, hiplib, monkeypatch, kind, n, chains, steps):
+    monkeypatch.setenv("MH_SPEC", "1")
+    room = _room(mh, kind, n)
+    seed = 5150 + n + chains
+    with mh.Session(room, chains, seed=seed) as s:
+        assert s.step_kernel() == (64, 4, "speculative")
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+        cur = s.current_costs()
+    ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
+    check_chains(f"speculative {kind} N={n}", pts, costs, ref_pts, ref_costs, report=True)
+    # the costs each chain carries equal the final pass's, OffLimits aside
+    keep = [0, 1, 2, 3, 4, 5, 7]
+    assert np.array_equal(cur[:, keep].view(np.uint32), costs[:, keep].view(np.uint32))
+
+
+def test_spec_resume_split_runs(mh, hiplib, monkeypatch):
+    """k runs of m steps equal one run of k m steps (the stream, the Box-Muller cache and the
+    accepted count resume exactly across batch and launch boundaries)."""
+    monkeypatch.setenv("MH_SPEC", "1")
+    room = mh.synthetic_room(8)
+    with mh.Session(room, 96, seed=77) as s:
+        for m in (1, 2, 3, 7, 8, 9, 13, 999, 1000, 1001):
+            s.run(m)
+        s.finalize()
+        p1, c1 = s.download()
+        a1 = s.summary().accepted
+    with mh.Session(room, 96, seed=77) as s:
+        s.run(3043)
+        s.finalize()
+        p2, c2 = s.download()
+        a2 = s.summary().accepted
+    assert np.array_equal(p1.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))
+    assert a1 == a2
+
+
+def test_spec_selection(mh, hiplib, monkeypatch):
+    """Opt-in with MH_SPEC=1, for the plain family and rooms of at most 8 objects only."""
+    monkeypatch.delenv("MH_DELTA", raising=False)
+    monkeypatch.delenv("MH_SPEC", raising=False)
+    with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
+        assert s.step_kernel()[2] != "speculative"
+    monkeypatch.setenv("MH_SPEC", "1")
+    with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
+        assert s.step_kernel()[2] == "speculative"
+    with mh.Session(mh.synthetic_room(8), 1024, seed=1, track=1) as s:  # (plain family only)
+        assert s.step_kernel()[2] != "speculative"
+    with mh.Session(mh.synthetic_room(16), 1024, seed=1) as s:
+        assert s.step_kernel()[2] != "speculative"

@@ -59,6 +59,7 @@ def one(kind, n, chains, steps, kernel):
     import __graft_entry__ as graft
     mh = graft.load_package()
     os.environ["MH_DELTA"] = "1" if kernel == "incremental" else "0"
+    os.environ["MH_SPEC"] = "0"  # (the speculative kernel takes no decision on the bound)
     lib = mh.load_library(str(LIB))
     mh.abi._lib = lib  # the Session wrapper uses the module's library
     room = room_of(mh, kind, n)

@@ -18,11 +18,14 @@ for M in "$@"; do
     check) DEF=-DMH_CHECK=1 ;;
     countsinl) DEF="-DMH_STAMPS=2 -DMH_EVAL_INLINE=1" ;;
     noinl) DEF=-DMH_EVAL_INLINE=-1 ;;
+    specdbg) DEF=-DMH_SPEC_DEBUG=1 ;;
+    ool*) DEF=-DMH_MATH_OOL=${M#ool} ;;
     wpe*) DEF=-DMH_WAVES_PER_EU=${M#wpe} ;;
     dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
     *) DEF=-DMH_ABLATE=$M ;;
   esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
-    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
+    -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip $C/mh_spec.hip \
+    $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
 done
 wait

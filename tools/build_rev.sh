@@ -11,6 +11,7 @@ for f in $(git ls-tree --name-only $REV metropolis-hastings-gpgpu_amd/csrc/) inc
 done
 C=$T/metropolis-hastings-gpgpu_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
-  -Wno-unused-result $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip $C/mh_abi.cpp \
+  -Wno-unused-result $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip \
+  $(test -f $C/mh_spec.hip && echo $C/mh_spec.hip) $C/mh_abi.cpp \
   -o ablate/libmhgpu_$NAME.so
 rm -rf $T
