@@ -304,9 +304,9 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
         if (*e) g.few = plain && g.L == 64 && g.npl <= 1 && atoi(e) != 0;
     // Rooms of at most 8 objects with too few chains to fill the GPU (the few-chains regime):
     // the speculative kernel evaluates 8 consecutive proposals per wavefront at once and commits
-    // up to the first accepted one. Opt-in ($MH_SPEC=1) while it is slower than OP_STEP_FEW at
-    // config 2 (round 4: 4.39 against 3.92 ms per launch).
-    g.spec = false;
+    // up to the first accepted one (config 2: 3.60 against OP_STEP_FEW's 3.95 ms per launch,
+    // profiles/r04/spec_vs_few.txt). $MH_SPEC=0/1 forces the choice.
+    g.spec = plain && mh::spec_fits(n, c, r) && n_chains <= 8LL * cus;
     if (const char* e = getenv("MH_SPEC"))
         if (*e) g.spec = plain && mh::spec_fits(n, c, r) && atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);

@@ -29,8 +29,8 @@ __device__ unsigned int g_spec_dbg_n;
 #define MH_STAMPS 0  // diagnostic builds: cycles per phase of a batch (tools/stamps.py)
 #endif
 #if MH_STAMPS
-// cycles of the phases of a batch, then batches and committed steps
-__device__ unsigned long long g_spec_cycles[10];
+// cycles of the phases of a batch (0-11), then batches and committed steps (14, 15)
+__device__ unsigned long long g_spec_cycles[16];
 #define SSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t) :: "memory"); cyc[k] += _t - t_last; t_last = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define SSTAMP(k) do { } while (0)
@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     unsigned int accepted = 0;
     const float rx_sx = rm.sx, rx_sy = rm.sy;
 #if MH_STAMPS
-    unsigned long long cyc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
+    unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
 #endif
 #pragma clang loop unroll(disable)
@@ -330,38 +330,41 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 pafter = (int)o;
             }
         }
-        // The walk: state (o, h, cache position: -1 = the batch's incoming cached normal).
+        SSTAMP(8);
+        // The walk: state (o, h, cache position: -1 = the batch's incoming cached normal), all
+        // wave-uniform (readfirstlane keeps it in scalar registers), branch-free: one readlane of
+        // the packed parse per hop.
+        const int pk = pmode | (pafter << 2);
         unsigned int go = off, gnext = off + 1;  // lanes of group s: step s's start and the next's
-        int gh = 0, gcp = -1;            // and step s's cache flag and position
-        unsigned int wo = off;
-        int wh = bmh, wcp = -1;
-        for (int s = 0; s < kb; ++s) {
-            const int i = (int)(wo - off);
-            const int md = i < 64 ? __builtin_amdgcn_readlane(pmode, i) : 3;
-            if (md == 3) {
-                kb = s;
-                break;
-            }
+        int gh = 0, gcp = -1;                    // and step s's cache flag and position
+        const unsigned int off_s = (unsigned int)__builtin_amdgcn_readfirstlane((int)off);
+        unsigned int wo = off_s;
+        int wh = __builtin_amdgcn_readfirstlane(bmh), wcp = -1;
+        int kw = __builtin_amdgcn_readfirstlane(kb);
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            const int i = __builtin_amdgcn_readfirstlane((int)(wo - off_s));
+            const int v = __builtin_amdgcn_readlane(pk, i & 63);
+            const int md = (i < 64 && s < kw) ? (v & 3) : 3;
+            kw = (md == 3 && s < kw) ? s : kw;
             go = g == s ? wo : go;
             gh = g == s ? wh : gh;
             gcp = g == s ? wcp : gcp;
-            const unsigned int pa = (unsigned int)__builtin_amdgcn_readlane(pafter, i);
-            if (md == 0) {  // translate
-                if (wh) wcp = (int)pa;
-                wo = pa + 3;
-            } else if (md == 1) {  // rotate
-                if (!wh) {
-                    wcp = (int)pa;
-                    wo = pa + 3;
-                } else {
-                    wo = pa + 1;
-                }
-                wh = !wh;
-            } else {  // swap
-                wo = pa + 1;
-            }
+            const int pa = v >> 2;
+            const bool tr = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
+            const bool pair = tr || (ro && !wh);    // the step takes a Box-Muller pair
+            wcp = (tr && wh) || (ro && !wh) ? pa : wcp;  // ... and caches its second
+            wo = md == 3 ? wo : (unsigned int)pa + (pair ? 3u : 1u);
+            wh = ro ? !wh : wh;
             gnext = g == s ? wo : gnext;
         }
+        kb = kw;
+        if (g >= kb) {  // (groups past the batch: harmless reads)
+            go = off;
+            gnext = off + 1;
+            gcp = -1;
+        }
+        SSTAMP(9);
         // Group g's step from lane (start - off)'s parse, its normals and Accept's uniform.
         SpecRec R;
         R.live = g < kb;
@@ -665,13 +668,13 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         done += committed;
         SSTAMP(7);
 #if MH_STAMPS
-        cyc[8] += 1;
-        cyc[9] += (unsigned long long)committed;
+        cyc[14] += 1;
+        cyc[15] += (unsigned long long)committed;
 #endif
     }
 #if MH_STAMPS
     if (lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
+        for (int k = 0; k < 16; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
 #endif
 
     if (lane < n) {
@@ -709,9 +712,9 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_spec(unsigned int
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_cycles), sizeof(unsigned long long) * 10) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_cycles), sizeof(unsigned long long) * 16) != hipSuccess)
         return -1;
-    unsigned long long zero[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long zero[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_spec_cycles), zero, sizeof(zero));
     return 0;
 }

@@ -79,16 +79,18 @@ def test_spec_resume_split_runs(mh, hiplib, monkeypatch):
     assert a1 == a2
 
 
-def test_spec_selection(mh, hiplib, monkeypatch):
-    """Opt-in with MH_SPEC=1, for the plain family and rooms of at most 8 objects only."""
-    monkeypatch.delenv("MH_DELTA", raising=False)
+def test_spec_is_the_default_for_few_small_chains(mh, hiplib, monkeypatch):
+    """The plain family, rooms of at most 8 objects, at most 8 chains per CU; MH_SPEC=0 opts out."""
     monkeypatch.delenv("MH_SPEC", raising=False)
-    with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
-        assert s.step_kernel()[2] != "speculative"
-    monkeypatch.setenv("MH_SPEC", "1")
+    monkeypatch.delenv("MH_DELTA", raising=False)
     with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
         assert s.step_kernel()[2] == "speculative"
     with mh.Session(mh.synthetic_room(8), 1024, seed=1, track=1) as s:  # (plain family only)
         assert s.step_kernel()[2] != "speculative"
     with mh.Session(mh.synthetic_room(16), 1024, seed=1) as s:
+        assert s.step_kernel()[2] != "speculative"
+    with mh.Session(mh.synthetic_room(8), 1 << 16, seed=1) as s:  # enough chains to fill the GPU
+        assert s.step_kernel()[2] != "speculative"
+    monkeypatch.setenv("MH_SPEC", "0")
+    with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
         assert s.step_kernel()[2] != "speculative"

@@ -13,12 +13,14 @@ sys.path.insert(0, str(ROOT))
 os.environ.setdefault("MH_LIB", str(ROOT / "ablate" / "libmhgpu_stamps.so"))
 import __graft_entry__ as graft  # noqa: E402
 
-DELTA_SPEC_PHASES = ["refill", "scan proposals", "apply + views", "per-object exact terms",
-               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit"]
+DELTA_SPEC_PHASES = ["refill", "scan: group records", "apply + views", "per-object exact terms",
+               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
+               "scan: lane parse", "scan: walk", "", ""]
 PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
-SPEC_PHASES = ["refill", "scan proposals", "apply + views", "per-object exact terms",
-               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit"]
+SPEC_PHASES = ["refill", "scan: group records", "apply + views", "per-object exact terms",
+               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
+               "scan: lane parse", "scan: walk", "", ""]
 PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
           "E SA walk + CL list", "F PW/ANG + replay", "accept/undo"]
 
@@ -46,11 +48,13 @@ def main():
     out = (C.c_ulonglong * 16)()
     if s_kind == "speculative":  # one chain per wavefront, per-batch phases
         assert lib.mh_debug_spec_cycles(out) == 0
-        tot = sum(out[:8])
-        batches, steps = out[8], out[9]
+        tot = sum(out[:12])
+        batches, steps = out[14], out[15]
         print(f"N={n} chains={chains} iters={iters} speculative acceptance={acc_rate:.4f} "
               f"steps per batch {steps / max(1, batches):.3f}")
-        for name, v in zip(SPEC_PHASES, out[:8]):
+        for name, v in zip(SPEC_PHASES, out[:12]):
+            if not name:
+                continue
             print(f"  {name:24s} {100.0 * v / tot:6.2f}%   {v / max(1, batches):10.1f} cycles/batch"
                   f"   {v / max(1, steps):10.1f} cycles/step")
         return
