@@ -13,6 +13,9 @@
 #include "mh_launch.h"
 #include "mh_math.h"
 
+#ifndef MH_ABLATE_OCML
+#define MH_ABLATE_OCML 0  // timing-only builds: the device library's transcendentals (results differ)
+#endif
 #ifndef MH_ABLATE
 #define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
 #endif
@@ -107,10 +110,18 @@ __device__ __forceinline__ float2 box_muller_inl(unsigned int a, unsigned int b)
     if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
     const double u1 = (double)a * 0x1p-32 + 0x1p-33;
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
+#if MH_ABLATE_OCML
+    const double rad = sqrt(-2.0 * ::log(u1));
+#else
     const double rad = sqrt(-2.0 * mh_log(u1));
+#endif
     const double ang = 6.283185307179586 * u2;
     double s, c;
+#if MH_ABLATE_OCML
+    ::sincos(ang, &s, &c);
+#else
     mh_sincos_medium(ang, &s, &c);  // (one argument reduction for both; ang < 2 pi)
+#endif
     return make_float2((float)(rad * s), (float)(rad * c));
 }
 
@@ -476,9 +487,15 @@ __device__ __forceinline__ double distance_f(float xi, float yi, float xj, float
 #else
 #define MH_OOL_KIND4 always_inline
 #endif
+#if MH_ABLATE_OCML  // timing-only ablation: the device library's functions (results differ)
+static __device__ MH_OOL_ATTR(1) double atan2_ool(double y, double x) { return ::atan2(y, x); }
+static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return ::cosf(x); }
+static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return ::exp(x); }
+#else
 static __device__ MH_OOL_ATTR(1) double atan2_ool(double y, double x) { return mh_atan2(y, x); }
 static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return mh_cos_f32(x); }
 static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return mh_exp(x); }
+#endif
 
 // Kernel.cu:170-182.
 __device__ __forceinline__ double theta_f(float xi, float yi, float xj, float yj, float ti) {

@@ -380,6 +380,43 @@ MH_MATH_FN double mh_atan(double x) {
          : id < 0 ? small : big;
 }
 
+/* atan(a / b) for finite a, b > 0 (hm: the larger high word), with one division: fdlibm's
+ * reduction of t = a / b, (t - c) / (1 + c t), applied to the operands as (a - c b) / (b + c a)
+ * (exact numerators by Sterbenz for c = 1/2, 1; one fma rounding for c = 3/2), then fdlibm's
+ * polynomial and atanhi/atanlo. The interval of t is chosen by comparing a with multiples of b
+ * (either interval is accurate near a boundary). Operands near overflow or in the subnormal
+ * range are scaled by a power of two first, which leaves the ratio unchanged. */
+MH_MATH_FN double mh_atan_ratio(double a, double b, uint32_t hm) {
+    const double atanhi0 = 4.63647609000806093515e-01, atanhi1 = 7.85398163397448278999e-01,
+                 atanhi2 = 9.82793723247329054082e-01, atanhi3 = 1.57079632679489655800e+00;
+    const double atanlo0 = 2.26987774529616870924e-17, atanlo1 = 3.06161699786838301793e-17,
+                 atanlo2 = 1.39033110312309984516e-17, atanlo3 = 6.12323399573676603587e-17;
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const double sc = hm >= 0x7FC00000u ? 0.25 : hm < 0x00300000u ? 0x1p54 : 1.0;
+    a = a * sc;
+    b = b * sc;
+    /* id: -1 for t below 7/16, 0 below 11/16, 1 below 19/16, 2 below 39/16, 3 above */
+    const int id = a < 0.4375 * b ? -1 : a < 0.6875 * b ? 0 : a < 1.1875 * b ? 1
+                 : a < 2.4375 * b ? 2 : 3;
+    const double num = id < 0 ? a : id == 0 ? 2.0 * a - b : id == 1 ? a - b
+                     : id == 2 ? __builtin_fma(-1.5, b, a) : -b;
+    const double den = id < 0 ? b : id == 0 ? 2.0 * b + a : id == 1 ? a + b
+                     : id == 2 ? __builtin_fma(1.5, a, b) : a;
+    const double t = num / den;
+    const double hi = id < 0 ? 0.0 : id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
+    const double lo = id < 0 ? 0.0 : id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+    const double z = t * t;
+    const double w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    return id < 0 ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+}
+
 /* atan2 (e_atan2.c): the special operands (NaN, zeros, infinities) on a branch of their own;
  * the general case as selects over atan(|y / x|). (fdlibm's x == 1 shortcut, atan(y), returns
  * the general case's value -- for |y| > 2^60 both round to pi/2 -- so it is not taken.) */
@@ -420,7 +457,7 @@ MH_MATH_FN double mh_atan2(double y, double x) {
     const int k = ((int)iy - (int)ix) >> 20;
     const int big = k > 60;                                  /* |y / x| > 2^60 */
     const int tiny = !big && (ux >> 63) && k < -60;          /* 0 > |y| / x > -2^-60 */
-    const double at = mh_atan(__builtin_fabs(y / x));
+    const double at = mh_atan_ratio(__builtin_fabs(y), __builtin_fabs(x), ix > iy ? ix : iy);
     const double z = big ? pi_o_2 + 0.5 * pi_lo : tiny ? 0.0 : at;
     const int mm = big ? (m & 1) : m;
     return mm == 0 ? z : mm == 1 ? -z : mm == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
