@@ -70,6 +70,61 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- cross-lane LDS hand-offs -------------------------------------------------------------
+// LDS that some lanes of a wavefront write and other lanes read changes hands in phases (round
+// 3 lost chains to a missing wave_sync after a one-lane store). Lanes write through a Staged<T>
+// view (put only); publish() -- which holds the wave_sync -- returns Published<T> views (reads
+// only) of the arrays it is given; restage() turns a published array back into a staged one
+// (also a wave_sync: every lane's reads are done before any lane rewrites). A cross-lane read
+// with no publish() between it and the writes does not compile. (The speculative kernel is
+// written this way; the older kernels keep explicit wave_sync() calls, checked by the parity
+// suite.)
+template <class T>
+struct Published {
+    const T* p;
+    __device__ __forceinline__ const T& operator[](int i) const { return p[i]; }
+    __device__ __forceinline__ const T* ptr() const { return p; }
+};
+template <class T>
+struct Staged {
+    T* p;
+    __device__ __forceinline__ void put(int i, const T& v) const { p[i] = v; }
+    __device__ __forceinline__ Staged<T> at(int off) const { return Staged<T>{p + off}; }
+};
+// publish(a, ...): one wave_sync, then the arrays' read views (`auto [av, bv] = publish(a, b);`).
+template <class A, class B>
+struct Pub2 { Published<A> a; Published<B> b; };
+template <class A, class B, class C>
+struct Pub3 { Published<A> a; Published<B> b; Published<C> c; };
+template <class A>
+__device__ __forceinline__ Published<A> publish(const Staged<A>& a) {
+    wave_sync();
+    return Published<A>{a.p};
+}
+template <class A, class B>
+__device__ __forceinline__ Pub2<A, B> publish(const Staged<A>& a, const Staged<B>& b) {
+    wave_sync();
+    return Pub2<A, B>{{a.p}, {b.p}};
+}
+template <class A, class B, class C>
+__device__ __forceinline__ Pub3<A, B, C> publish(const Staged<A>& a, const Staged<B>& b,
+                                                 const Staged<C>& c) {
+    wave_sync();
+    return Pub3<A, B, C>{{a.p}, {b.p}, {c.p}};
+}
+template <class T>
+__device__ __forceinline__ Staged<T> restage(const Published<T>& v) {
+    wave_sync();
+    return Staged<T>{const_cast<T*>(v.p)};
+}
+template <class A, class B, class C>
+struct Stg3 { Staged<A> a; Staged<B> b; Staged<C> c; };
+template <class A, class B, class C>
+__device__ __forceinline__ Stg3<A, B, C> restage(const Pub3<A, B, C>& v) {
+    wave_sync();
+    return Stg3<A, B, C>{{const_cast<A*>(v.a.p)}, {const_cast<B*>(v.b.p)}, {const_cast<C*>(v.c.p)}};
+}
+
 template <int L>
 __device__ __forceinline__ uint64_t group_ballot(bool pred, int gbase) {
     uint64_t b = __ballot(pred);

@@ -151,17 +151,18 @@ __device__ __forceinline__ float sym_row(const ObjP* P, const double* RY, int n,
 // Appends the non-zero components of t (when `on`), in lane order within each group, to the
 // group's stream at `pos` (pre-negated: the reference subtracts them); advances pos by the
 // group's count.
-__device__ __forceinline__ void append4(double* S, int& pos, float4 t, bool on, int r) {
+__device__ __forceinline__ void append4(const Staged<double>& S, int& pos, float4 t, bool on,
+                                        int r) {
     const int cnt = on ? (int)(t.x != 0.0f) + (int)(t.y != 0.0f) + (int)(t.z != 0.0f) +
                              (int)(t.w != 0.0f)
                        : 0;
     int tot;
     int q = pos + group_excl_scan<GL>(cnt, r, tot);
     if (on) {
-        if (t.x != 0.0f) S[q++] = -(double)t.x;
-        if (t.y != 0.0f) S[q++] = -(double)t.y;
-        if (t.z != 0.0f) S[q++] = -(double)t.z;
-        if (t.w != 0.0f) S[q++] = -(double)t.w;
+        if (t.x != 0.0f) S.put(q++, -(double)t.x);
+        if (t.y != 0.0f) S.put(q++, -(double)t.y);
+        if (t.z != 0.0f) S.put(q++, -(double)t.z);
+        if (t.w != 0.0f) S.put(q++, -(double)t.w);
     }
     pos += tot;
 }
@@ -211,26 +212,34 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 
     // The current configuration's per-object and per-relationship terms (carried across
     // steps; a proposal recomputes the ones it changes).
+    // (LDS shared between lanes moves through Staged / Published views, mh_common.h)
+    const Staged<ObjP> Pst{X->P[g]};
+    const Staged<double> RYst{X->RY[g]};
+    const Staged<double> Sst{X->S[g]};
+    const Staged<float4> CLBst{X->CLB[g]};
+    const Staged<double> SUMst{X->SUM[g]};
     if (r < n) {
         ObjP p;
         p.xf = (float)cx;
         p.yf = (float)cy;
         p.rotYf = (float)cry;
         p.pad = 0.0f;
-        X->P[g][r] = p;
-        X->RY[g][r] = cry;
+        Pst.put(r, p);
+        RYst.put(r, cry);
     }
-    wave_sync();
+    const Published<ObjP> P0 = publish(Pst);
     float cph = 0.0f;
     double rpw0 = 0.0, rang0 = 0.0, rpw1 = 0.0, rang1 = 0.0;
     if (r < n) cph = focal_cos(rm, (float)cx, (float)cy, (float)cry);
-    if (r < nr) rel_exact(H->rel[r], X->P[g], rpw0, rang0);
-    if (r + GL < nr) rel_exact(H->rel[r + GL], X->P[g], rpw1, rang1);
+    if (r < nr) rel_exact(H->rel[r], P0.ptr(), rpw0, rang0);
+    if (r + GL < nr) rel_exact(H->rel[r + GL], P0.ptr(), rpw1, rang1);
 
     // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i holds
     // words start + i and start + 64 + i; LDS the words and the Box-Muller pairs of both.
     const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
     uint64_t wbase = 0;
+    // the window: words, then the Box-Muller pairs' first and second normals
+    Pub3<unsigned int, float, float> win{{X->wd}, {X->bs}, {X->bc}};
     auto fill = [&](uint64_t at) __attribute__((always_inline)) {
         wbase = at;
         const unsigned int w0 = philox_word(seed, sub, at + (uint64_t)lane);
@@ -243,14 +252,14 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         const unsigned int n1 = (unsigned int)__shfl_down((int)w1, 1);  // (lane 63's unused)
         const float2 z0 = box_muller_inl(w0, n0);
         const float2 z1 = box_muller_inl(w1, n1);
-        wave_sync();  // (every lane's reads of the previous window are done)
-        X->wd[lane] = w0;
-        X->wd[64 + lane] = w1;
-        X->bs[lane] = z0.x;
-        X->bc[lane] = z0.y;
-        X->bs[64 + lane] = z1.x;
-        X->bc[64 + lane] = z1.y;
-        wave_sync();
+        const auto w = restage(win);  // (every lane's reads of the previous window are done)
+        w.a.put(lane, w0);
+        w.a.put(64 + lane, w1);
+        w.b.put(lane, z0.x);
+        w.c.put(lane, z0.y);
+        w.b.put(64 + lane, z1.x);
+        w.c.put(64 + lane, z1.y);
+        win = publish(w.a, w.b, w.c);
     };
     fill(m0.draws);
     unsigned int off = 0;  // next draw - window start (wave-uniform)
@@ -258,7 +267,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     float bmv = m0.bm_val;
     // Draws at a lane's own offset (every lane may read a different one).
     auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
-        return o < 128 ? X->wd[o] : philox_far(seed, sub, wbase + o);
+        return o < 128 ? win.a[o] : philox_far(seed, sub, wbase + o);
     };
     auto uni_v = [&](unsigned int& o) __attribute__((always_inline)) {
         return rocrand_device::detail::uniform_distribution(word_v(o++));
@@ -282,7 +291,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     };
     // The Box-Muller pair (word p, word p + 1): the window's table, or computed past it.
     auto pair_v = [&](unsigned int p) __attribute__((always_inline)) -> float2 {
-        if (p < 127) return make_float2(X->bs[p], X->bc[p]);
+        if (p < 127) return make_float2(win.b[p], win.c[p]);
         return box_muller_inl(word_v(p), word_v(p + 1));
     };
 
@@ -314,7 +323,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         {
             const unsigned int o0 = off + (unsigned int)lane;
             if (o0 < 124) {
-                const unsigned int wa = X->wd[o0], wb = X->wd[o0 + 1], wc = X->wd[o0 + 2];
+                const unsigned int wa = win.a[o0], wb = win.a[o0 + 1], wc = win.a[o0 + 2];
                 unsigned int o = o0 + 1;
                 pmode = rand_w(wa, 2);
                 if (pmode != 2 || n >= 2) {
@@ -376,8 +385,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             R.k1 = __builtin_amdgcn_ds_bpermute(src, pk1);
             R.k2 = __builtin_amdgcn_ds_bpermute(src, pk2);
             const unsigned int pa = (unsigned int)__builtin_amdgcn_ds_bpermute(src, pafter);
-            const float2 z = make_float2(X->bs[pa < 127 ? pa : 0], X->bc[pa < 127 ? pa : 0]);
-            const float bv = gcp < 0 ? bmv : X->bc[gcp < 127 ? gcp : 0];
+            const float2 z = make_float2(win.b[pa < 127 ? pa : 0], win.c[pa < 127 ? pa : 0]);
+            const float bv = gcp < 0 ? bmv : win.c[gcp < 127 ? gcp : 0];
             const unsigned int wu = word_v(gnext - 1);
             float zs = z.x, zc = z.y, bvi = bv;
             if (__builtin_expect(pa >= 127 || gcp >= 127, 0)) {  // pairs past the table
@@ -455,12 +464,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             p.yf = yf;
             p.rotYf = ryf;
             p.pad = 0.0f;
-            X->P[g][r] = p;
-            X->RY[g][r] = sry;
+            Pst.put(r, p);
+            RYst.put(r, sry);
         }
-        wave_sync();
+        const auto pv = publish(Pst, RYst);
         SSTAMP(2);
-        const ObjP* Pg = X->P[g];
+        const ObjP* Pg = pv.a.ptr();
 
         // Per-object terms of the proposal's configuration.
         float cphs = cph;
@@ -503,9 +512,9 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         if (r < n) {
             const RectShape os = H->objs[r];
             const float area = __int_as_float(os.pad);
-            X->S[g][S_VBX + r] = (double)area * sx;  // Kernel.cu:200-201
-            X->S[g][S_VBY + r] = (double)area * sy;
-            X->S[g][S_FP + r] = -(double)cphs;
+            Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
+            Sst.put(S_VBY + r, (double)area * sy);
+            Sst.put(S_FP + r, -(double)cphs);
             box = shape_box(os, xf, yf);
             sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
             wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
@@ -513,16 +522,16 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         if (r < c) {
             const RectShape cs = H->clrs[r];
             const ObjP ps = Pg[cs.pad];
-            X->CLB[g][r] = shape_box(cs, ps.xf, ps.yf);     // Clearance, :414-415
+            CLBst.put(r, shape_box(cs, ps.xf, ps.yf));      // Clearance, :414-415
             sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
         }
         if (r < nr) {
-            X->S[g][S_PW + r] = -pw0;
-            X->S[g][S_ANG + r] = -an0;
+            Sst.put(S_PW + r, -pw0);
+            Sst.put(S_ANG + r, -an0);
         }
         if (r + GL < nr) {
-            X->S[g][S_PW + r + GL] = -pw1;
-            X->S[g][S_ANG + r + GL] = -an1;
+            Sst.put(S_PW + r + GL, -pw1);
+            Sst.put(S_ANG + r + GL, -an1);
         }
         // Symmetry row r, Kernel.cu:292-312.
         const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
@@ -534,22 +543,22 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             const float ryr = (float)(sy + (double)(sd * rm.uy));
             float rr = (float)(rm.two_focal_rot - sry);
             if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
-            best = sym_row(Pg, X->RY[g], n, rxr, ryr, rr, exact_mode);
-            X->S[g][S_SYM + r] = -(double)best;
+            best = sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode);
+            Sst.put(S_SYM + r, -(double)best);
         }
-        wave_sync();
+        const auto sv = publish(Sst, CLBst);  // (the streams so far are read by the replay)
         SSTAMP(4);
         // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
         // (clearances, then objects, :445-480), compacted in the reference's order.
         int ncl = 0, nsa = 0;
         for (int i = 0; i < c; ++i) {
             float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < n) t4.x = overlap(X->CLB[g][i], box);
-            append4(&X->S[g][S_CL], ncl, t4, r < n, r);
+            if (r < n) t4.x = overlap(sv.b[i], box);
+            append4(Sst.at(S_CL), ncl, t4, r < n, r);
         }
-        append4(&X->S[g][S_SA], nsa, sac, r < c, r);
-        append4(&X->S[g][S_SA], nsa, sao, r < n, r);
-        wave_sync();
+        append4(Sst.at(S_SA), nsa, sac, r < c, r);
+        append4(Sst.at(S_SA), nsa, sao, r < n, r);
+        const Published<double> Sv = publish(Sst);
         SSTAMP(5);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
         // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2).
@@ -566,20 +575,20 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 case 6: base = S_PW; len = nr; rnd = false; break;
                 default: base = S_ANG; len = nr; rnd = false; break;
             }
-            const double* src = &X->S[g][base];
+            const double* src = Sv.ptr() + base;
             double acc = 0.0;
             for (int l = 0; l < len; ++l) {
                 const double s = acc + src[l];
                 acc = rnd ? (double)(float)s : s;
             }
-            X->SUM[g][r] = acc;
+            SUMst.put(r, acc);
         }
-        wave_sync();
+        const Published<double> SUMv = publish(SUMst);
         SSTAMP(6);
         // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547).
         float sc[8];
         {
-            const double* sm = X->SUM[g];
+            const double* sm = SUMv.ptr();
             const float nx = (float)sm[0], ny = (float)sm[1];
             const double fpd = sm[2];
             const float symf = (float)sm[3], clf = (float)sm[4], saf = (float)sm[5];
