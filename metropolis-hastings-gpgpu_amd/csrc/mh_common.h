@@ -14,7 +14,8 @@
 #include "mh_math.h"
 
 #ifndef MH_ABLATE_OCML
-#define MH_ABLATE_OCML 0  // timing-only builds: the device library's transcendentals (results differ)
+#define MH_ABLATE_OCML 0  // timing-only builds: bit mask of the transcendentals taken from the
+                          // device library (1 Box-Muller, 2 atan2, 4 cosf, 8 exp; results differ)
 #endif
 #ifndef MH_ABLATE
 #define MH_ABLATE 0  // timing-only builds (tools/build_ablate.sh) compile phases out; product = 0
@@ -165,14 +166,14 @@ __device__ __forceinline__ float2 box_muller_inl(unsigned int a, unsigned int b)
     if (MH_ABLATE & 32) return make_float2((float)(a >> 8) * 0x1p-24f - 0.5f, (float)(b >> 8) * 0x1p-24f - 0.5f);
     const double u1 = (double)a * 0x1p-32 + 0x1p-33;
     const double u2 = (double)b * 0x1p-32 + 0x1p-33;
-#if MH_ABLATE_OCML
+#if MH_ABLATE_OCML & 1
     const double rad = sqrt(-2.0 * ::log(u1));
 #else
     const double rad = sqrt(-2.0 * mh_log(u1));
 #endif
     const double ang = 6.283185307179586 * u2;
     double s, c;
-#if MH_ABLATE_OCML
+#if MH_ABLATE_OCML & 1
     ::sincos(ang, &s, &c);
 #else
     mh_sincos_medium(ang, &s, &c);  // (one argument reduction for both; ang < 2 pi)
@@ -542,13 +543,19 @@ __device__ __forceinline__ double distance_f(float xi, float yi, float xj, float
 #else
 #define MH_OOL_KIND4 always_inline
 #endif
-#if MH_ABLATE_OCML  // timing-only ablation: the device library's functions (results differ)
+#if MH_ABLATE_OCML & 2  // timing-only ablations: the device library's functions (results differ)
 static __device__ MH_OOL_ATTR(1) double atan2_ool(double y, double x) { return ::atan2(y, x); }
-static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return ::cosf(x); }
-static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return ::exp(x); }
 #else
 static __device__ MH_OOL_ATTR(1) double atan2_ool(double y, double x) { return mh_atan2(y, x); }
+#endif
+#if MH_ABLATE_OCML & 4
+static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return ::cosf(x); }
+#else
 static __device__ MH_OOL_ATTR(2) float cos_f32_ool(float x) { return mh_cos_f32(x); }
+#endif
+#if MH_ABLATE_OCML & 8
+static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return ::exp(x); }
+#else
 static __device__ MH_OOL_ATTR(4) double exp_ool(double x) { return mh_exp(x); }
 #endif
 

@@ -34,6 +34,13 @@
 #define MH_MATH_FN static inline __attribute__((always_inline))
 #define MH_MATH_TABLE static const
 #endif
+/* A select whose condition varies between lanes: evaluated as a select, never as a branch (clang
+ * otherwise turns chains of such ternaries into divergent control flow on the GPU). */
+#if defined(__clang__)
+#define MH_SEL(c) __builtin_unpredictable(c)
+#else
+#define MH_SEL(c) (c)
+#endif
 
 /* ---- bit access ---------------------------------------------------------------------------- */
 
@@ -100,7 +107,8 @@ MH_MATH_FN double mh_log(double x) {
 
 /* ---- exp (fdlibm e_exp.c) -------------------------------------------------------------------
  * x = k ln2 + r, |r| <= ln2 / 2 (ln2 in two parts, so hi - lo is r to ~2^-85); exp(r) from the
- * degree-5 Remez approximation R(r^2) of r (e^r + 1) / (e^r - 1) (|error| < 2^-59), then 2^k. */
+ * degree-5 Remez approximation R(r^2) of r (e^r + 1) / (e^r - 1) (|error| < 2^-59; Horner with
+ * fused multiply-adds), then 2^k. */
 MH_MATH_FN double mh_exp(double x) {
     const double o_threshold = 7.09782712893383973096e+02, u_threshold = -7.45133219101941108420e+02;
     const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
@@ -125,32 +133,39 @@ MH_MATH_FN double mh_exp(double x) {
     const int kn = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
     const int k = !red ? 0 : near1 ? 1 - xsb - xsb : kn;
     const double tk = (double)kn;
-    const double hi = !red ? x : near1 ? (xsb ? x + ln2HI : x - ln2HI) : x - tk * ln2HI;
-    const double lo = !red ? 0.0 : near1 ? (xsb ? -ln2LO : ln2LO) : tk * ln2LO;
-    const double r = red ? hi - lo : x;
+    /* (every arm computed beforehand: a ternary with computed arms becomes a branch) */
+    const double hp = x + ln2HI, hm = x - ln2HI, hk = x - tk * ln2HI, lk = tk * ln2LO;
+    const double h1 = MH_SEL(xsb) ? hp : hm, l1 = MH_SEL(xsb) ? -ln2LO : ln2LO;
+    const double h2 = MH_SEL(near1) ? h1 : hk, l2 = MH_SEL(near1) ? l1 : lk;
+    const double hi = MH_SEL(red) ? h2 : x, lo = MH_SEL(red) ? l2 : 0.0;
+    const double rr = hi - lo;
+    const double r = MH_SEL(red) ? rr : x;
     const double t = r * r;
-    const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    const double c = __builtin_fma(-t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, P5, P4), P3), P2), P1), r);
     const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
     /* y 2^k: in one step for -1021 <= k < 1024, else in two */
-    const double f1 = k == 1024 ? 2.0 : k >= -1021 ? mh_pow2(k < 1023 ? k : 1023)
-                    : mh_pow2(k + 1000 > -1022 ? k + 1000 : -1022);
-    const double f2 = k == 1024 ? mh_pow2(1023) : k >= -1021 ? 1.0 : mh_pow2(-1000);
-    const double e = (y * f1) * f2;
-    return hx < 0x3E300000u ? 1.0 + x : e;       /* |x| < 2^-28 */
+    const double pa = mh_pow2(k < 1023 ? k : 1023), pb = mh_pow2(k + 1000 > -1022 ? k + 1000 : -1022);
+    const double fa = MH_SEL(k >= -1021) ? pa : pb;
+    const double f1 = MH_SEL(k == 1024) ? 2.0 : fa;
+    const double fb = MH_SEL(k >= -1021) ? 1.0 : mh_pow2(-1000);
+    const double f2 = MH_SEL(k == 1024) ? mh_pow2(1023) : fb;
+    const double e = (y * f1) * f2, e1 = 1.0 + x;
+    return MH_SEL(hx < 0x3E300000u) ? e1 : e;    /* |x| < 2^-28 */
 }
 
 /* ---- sin and cos ------------------------------------------------------------------------------ */
 
 /* fdlibm k_sin.c / k_cos.c (FreeBSD revision): sin and cos of x + y, |x + y| <= ~pi/4, y the
- * tail of the reduced argument. Minimax polynomials, |error| < 2^-58. */
+ * tail of the reduced argument. Minimax polynomials, |error| < 2^-58, evaluated with fused
+ * multiply-adds (round 4: fewer operations; the same on both sides, as fma is correctly rounded). */
 MH_MATH_FN double mh_ksin(double x, double y) {
     const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                  S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                  S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
     const double z = x * x;
     const double v = z * x;
-    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+    const double r = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, S6, S5), S4), S3), S2);
+    return x - __builtin_fma(-v, S1, __builtin_fma(z, __builtin_fma(-v, r, 0.5 * y), -y));
 }
 MH_MATH_FN double mh_kcos(double x, double y) {
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
@@ -158,10 +173,11 @@ MH_MATH_FN double mh_kcos(double x, double y) {
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
     const double z = x * x;
     const double w = z * z;
-    const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    const double r = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, C3, C2), C1),
+                                   (w * w) * __builtin_fma(z, __builtin_fma(z, C6, C5), C4));
     const double hz = 0.5 * z;
     const double w1 = 1.0 - hz;
-    return w1 + (((1.0 - w1) - hz) + (z * r - x * y));
+    return w1 + (((1.0 - w1) - hz) + __builtin_fma(z, r, -(x * y)));
 }
 
 /* 2/pi to 1280 bits: word k holds bits 32k+1 .. 32k+32 after the binary point (generated with
@@ -299,8 +315,11 @@ MH_MATH_FN int mh_rem_pio2_medium(double x, double* y0, double* y1) {
 /* sin and cos of the reduced argument in quadrant n */
 MH_MATH_FN void mh_sincos_q(int n, double y0, double y1, double* s, double* c) {
     const double ks = mh_ksin(y0, y1), kc = mh_kcos(y0, y1);
-    *s = n == 0 ? ks : n == 1 ? kc : n == 2 ? -ks : -kc;
-    *c = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
+    const double nks = -ks, nkc = -kc;
+    const double s01 = MH_SEL(n == 0) ? ks : kc, s23 = MH_SEL(n == 2) ? nks : nkc;
+    const double c01 = MH_SEL(n == 0) ? kc : nks, c23 = MH_SEL(n == 2) ? nkc : ks;
+    *s = MH_SEL(n < 2) ? s01 : s23;
+    *c = MH_SEL(n < 2) ? c01 : c23;
 }
 
 /* sin and cos of |x| <= 2^20 pi/2: the Box-Muller angles, which lie in (0, 2 pi] (the same values
@@ -319,8 +338,9 @@ MH_MATH_FN void mh_sincos(double x, double* s, double* c) {
         return;
     }
     double y0, y1;
-    const int n = ix > 0x413921FBu ? mh_rem_pio2_large(x, &y0, &y1)
-                                   : mh_rem_pio2_medium(x, &y0, &y1);
+    /* the medium reduction always (of 0 above its range), the large one only where needed */
+    int n = mh_rem_pio2_medium(ix > 0x413921FBu ? 0.0 : x, &y0, &y1);
+    if (ix > 0x413921FBu) n = mh_rem_pio2_large(x, &y0, &y1);
     mh_sincos_q(n, y0, y1, s, c);
 }
 
@@ -383,7 +403,7 @@ MH_MATH_FN double mh_atan(double x) {
 /* atan(a / b) for finite a, b > 0 (hm: the larger high word), with one division: fdlibm's
  * reduction of t = a / b, (t - c) / (1 + c t), applied to the operands as (a - c b) / (b + c a)
  * (exact numerators by Sterbenz for c = 1/2, 1; one fma rounding for c = 3/2), then fdlibm's
- * polynomial and atanhi/atanlo. The interval of t is chosen by comparing a with multiples of b
+ * polynomial (Horner with fused multiply-adds) and atanhi/atanlo. The interval of t is chosen by comparing a with multiples of b
  * (either interval is accurate near a boundary). Operands near overflow or in the subnormal
  * range are scaled by a power of two first, which leaves the ratio unchanged. */
 MH_MATH_FN double mh_atan_ratio(double a, double b, uint32_t hm) {
@@ -400,21 +420,26 @@ MH_MATH_FN double mh_atan_ratio(double a, double b, uint32_t hm) {
     const double sc = hm >= 0x7FC00000u ? 0.25 : hm < 0x00300000u ? 0x1p54 : 1.0;
     a = a * sc;
     b = b * sc;
-    /* id: -1 for t below 7/16, 0 below 11/16, 1 below 19/16, 2 below 39/16, 3 above */
-    const int id = a < 0.4375 * b ? -1 : a < 0.6875 * b ? 0 : a < 1.1875 * b ? 1
-                 : a < 2.4375 * b ? 2 : 3;
-    const double num = id < 0 ? a : id == 0 ? 2.0 * a - b : id == 1 ? a - b
-                     : id == 2 ? __builtin_fma(-1.5, b, a) : -b;
-    const double den = id < 0 ? b : id == 0 ? 2.0 * b + a : id == 1 ? a + b
-                     : id == 2 ? __builtin_fma(1.5, a, b) : a;
-    const double t = num / den;
-    const double hi = id < 0 ? 0.0 : id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
-    const double lo = id < 0 ? 0.0 : id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+    /* id: -1 for t below 7/16, 0 below 11/16, 1 below 19/16, 2 below 39/16, 3 above (the
+     * products are monotonic in the constant, so the comparisons can be summed);
+     * num = na a - nb b, den = nb a + na b (na in {0, 1}: the products are exact) */
+    const int id = -1 + (a >= 0.4375 * b) + (a >= 0.6875 * b) + (a >= 1.1875 * b) + (a >= 2.4375 * b);
+    const int e3 = id == 3;
+    const double nb = MH_SEL(e3) ? 1.0 : 0.5 * (double)(id + 1);  /* 0, 1/2, 1, 3/2, 1 */
+    const double na = MH_SEL(e3) ? 0.0 : 1.0;
+    const double t = __builtin_fma(-nb, b, na * a) / __builtin_fma(nb, a, na * b);
+    /* (every arm a value computed beforehand: a ternary with computed arms becomes a branch) */
+    const double h0 = MH_SEL(id < 0) ? 0.0 : atanhi0, h1 = MH_SEL(id < 2) ? atanhi1 : atanhi2;
+    const double h2 = MH_SEL(id < 3) ? h1 : atanhi3, hi = MH_SEL(id < 1) ? h0 : h2;
+    const double l0 = MH_SEL(id < 0) ? 0.0 : atanlo0, l1 = MH_SEL(id < 2) ? atanlo1 : atanlo2;
+    const double l2 = MH_SEL(id < 3) ? l1 : atanlo3, lo = MH_SEL(id < 1) ? l0 : l2;
     const double z = t * t;
     const double w = z * z;
-    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    return id < 0 ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+    const double s1 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, aT10, aT8), aT6), aT4), aT2), aT0);
+    const double s2 = w * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, aT9, aT7), aT5), aT3), aT1);
+    const double q = s1 + s2;
+    const double rs = __builtin_fma(-t, q, t), rb = hi - (__builtin_fma(t, q, -lo) - t);
+    return MH_SEL(id < 0) ? rs : rb;
 }
 
 /* atan2 (e_atan2.c): the special operands (NaN, zeros, infinities) on a branch of their own;
@@ -458,9 +483,13 @@ MH_MATH_FN double mh_atan2(double y, double x) {
     const int big = k > 60;                                  /* |y / x| > 2^60 */
     const int tiny = !big && (ux >> 63) && k < -60;          /* 0 > |y| / x > -2^-60 */
     const double at = mh_atan_ratio(__builtin_fabs(y), __builtin_fabs(x), ix > iy ? ix : iy);
-    const double z = big ? pi_o_2 + 0.5 * pi_lo : tiny ? 0.0 : at;
+    const double zt = MH_SEL(tiny) ? 0.0 : at;
+    const double z = MH_SEL(big) ? pi_o_2 + 0.5 * pi_lo : zt;
     const int mm = big ? (m & 1) : m;
-    return mm == 0 ? z : mm == 1 ? -z : mm == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
+    const double zn = -z, zl = z - pi_lo;
+    const double q2 = pi - zl, q3 = zl - pi;
+    const double r01 = MH_SEL(mm == 0) ? z : zn, r23 = MH_SEL(mm == 2) ? q2 : q3;
+    return MH_SEL(mm < 2) ? r01 : r23;
 }
 
 /* ---- the float functions of the reference ----------------------------------------------------

@@ -22,6 +22,6 @@ bash tools/profile_box.sh $TAG/n256 --objects 256 --chains 32768 --steps 3 --war
 python tools/pmc_summary.py $OUT/n256 --kernel "mh_delta_kernel" --chains 32768 \
     --json $OUT/pmc_step_kernel_n256.json --profile profiles/${TAG}_pmc_step_kernel_n256.txt > $OUT/pmc_n256.txt || exit 1
 bash tools/profile_box.sh $TAG/n8 --objects 8 --chains 1024 --steps 3 --warmup 1 --iters 1000 --no-cpu-baseline --e2e-iters 0 || exit 1
-python tools/pmc_summary.py $OUT/n8 --kernel "mh_kernel<64, 1, 6>" --chains 1024 \
+python tools/pmc_summary.py $OUT/n8 --kernel "mh_spec_kernel" --chains 1024 \
     --json $OUT/pmc_step_kernel_n8.json --profile profiles/${TAG}_pmc_step_kernel_n8.txt > $OUT/pmc_n8.txt || exit 1
 cat $OUT/pmc_n64.txt $OUT/pmc_n256.txt $OUT/pmc_n8.txt | grep -E "hbm_bytes|valu_issue|insts_per_wave|duration|Scratch|wait_inst"

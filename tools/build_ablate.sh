@@ -19,7 +19,7 @@ for M in "$@"; do
     countsinl) DEF="-DMH_STAMPS=2 -DMH_EVAL_INLINE=1" ;;
     noinl) DEF=-DMH_EVAL_INLINE=-1 ;;
     specdbg) DEF=-DMH_SPEC_DEBUG=1 ;;
-    ocml) DEF=-DMH_ABLATE_OCML=1 ;;
+    ocml*) DEF=-DMH_ABLATE_OCML=${M#ocml} ;;
     ool*) DEF=-DMH_MATH_OOL=${M#ool} ;;
     wpe*) DEF=-DMH_WAVES_PER_EU=${M#wpe} ;;
     dbl*) DEF=-DMH_DOUBLE=${M#dbl} ;;
