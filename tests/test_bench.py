@@ -51,3 +51,10 @@ def test_nccl_with_too_few_gpus_fails_loudly():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "need 2 GPUs" in r.stderr
+
+
+def test_committed_pmc_records_are_stamped():
+    """Every committed PMC record carries the source hash of the library it profiled."""
+    for p in (ROOT / "profiles").glob("pmc_step_kernel_n*.json"):
+        d = json.loads(p.read_text())
+        assert d.get("srchash"), p.name
