@@ -960,7 +960,7 @@ MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* c
     if (!s) { set_error("NULL session"); return -1; }
     const int L = (s->geo.delta || s->geo.spec) ? 64 : s->geo.L;  // the step kernel's shape
     const int w = s->geo.spec ? mh::spec_waves() : s->geo.delta ? s->geo.dwaves : s->geo.waves;
-    if (lanes_per_chain) *lanes_per_chain = L;
+    if (lanes_per_chain) *lanes_per_chain = s->geo.spec ? 64 * mh::spec_waves_per_chain() : L;
     if (chains_per_workgroup) *chains_per_workgroup = w * (64 / L);
     if (incremental) *incremental = s->geo.spec ? 3 : s->geo.delta ? 1 : (s->geo.few ? 2 : 0);
     return 0;

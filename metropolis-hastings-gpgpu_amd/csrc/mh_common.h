@@ -113,6 +113,12 @@ __device__ __forceinline__ Pub3<A, B, C> publish(const Staged<A>& a, const Stage
     wave_sync();
     return Pub3<A, B, C>{{a.p}, {b.p}, {c.p}};
 }
+// The same between the wavefronts of a workgroup (the workgroup barrier instead).
+template <class A>
+__device__ __forceinline__ Published<A> publish_workgroup(const Staged<A>& a) {
+    __syncthreads();
+    return Published<A>{a.p};
+}
 template <class T>
 __device__ __forceinline__ Staged<T> restage(const Published<T>& v) {
     wave_sync();

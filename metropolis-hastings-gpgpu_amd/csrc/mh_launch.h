@@ -68,7 +68,8 @@ hipError_t launch_math(int fn, uint64_t start, uint64_t count, double* out, hipS
 // The speculative step kernel (mh_spec.hip): rooms of at most 8 objects and 16 relationships,
 // one chain per wavefront evaluating 8 consecutive proposals at once.
 bool spec_fits(int n, int c, int r);
-int spec_waves();
+int spec_waves();            // chains per workgroup of the speculative kernel
+int spec_waves_per_chain();  // its wavefronts per chain
 size_t spec_lds_bytes(int waves_per_wg);
 int spec_blocks_per_cu();
 hipError_t launch_spec(const LaunchArgs& a, hipStream_t s);

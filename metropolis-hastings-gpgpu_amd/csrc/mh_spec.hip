@@ -42,7 +42,13 @@ namespace {
 constexpr int GL = 8;          // lanes per group: the largest room this kernel serves
 constexpr int K = 8;           // groups: proposals evaluated per batch
 constexpr int RMAX = 2 * GL;   // relationship slots (two per lane)
-constexpr int kSpecWaves = 4;  // chains (wavefronts) per workgroup
+// Two wavefronts per chain (one workgroup): both locate and apply the batch's proposals; wave 0
+// then evaluates the exact FocalPoint and relationship terms and replays their sums, wave 1 the
+// symmetry rows and the Clearance / SurfaceArea lists and replays theirs; one workgroup barrier
+// hands the eight sums over. At one chain per SIMD (config 2) the step is latency-bound, and the
+// split both halves that critical path and puts two wavefronts on every SIMD.
+constexpr int kSplit = 2;      // wavefronts per chain
+constexpr int kSpecWaves = kSplit;
 
 // Each group's ordered-sum streams (doubles, pre-signed so that every sum is acc + term):
 // VisualBalance area x and area y (Kernel.cu:200-201), FocalPoint -cos(phi) (:277), Symmetry
@@ -57,13 +63,16 @@ struct SpecRec {  // one step's proposal (the draws of Kernel.cu:576-704, 710)
 };
 
 struct SpecChain {  // LDS of one chain
-    double S[K][S_END];    // each group's ordered-sum streams
-    double SUM[K][8];      // each group's eight sums
+    double S[K][S_END];    // each group's ordered-sum streams (this wavefront's)
     float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
     double RY[K][GL];      // each group's double rotY of every object (Symmetry, :305)
     ObjP P[K][GL];         // each group's float pose words
     unsigned int wd[128];    // the 128-word window of the Philox stream
     float bs[128], bc[128];  // Box-Muller pairs (word i, word i + 1) of the window
+};
+
+struct SpecShared {  // LDS of the chain shared by its two wavefronts
+    double SUM[2][K][8];  // each group's eight sums (double-buffered by batch parity)
 };
 
 struct SpecHdr {  // LDS of the workgroup: the room tables
@@ -74,6 +83,7 @@ struct SpecHdr {  // LDS of the workgroup: the room tables
 
 constexpr int kSpecHdrBytes = (int)((sizeof(SpecHdr) + 15) & ~(size_t)15);
 constexpr int kSpecChainBytes = (int)((sizeof(SpecChain) + 15) & ~(size_t)15);
+constexpr int kSpecSharedBytes = (int)((sizeof(SpecShared) + 15) & ~(size_t)15);
 
 // A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
 __device__ __attribute__((noinline)) unsigned int philox_far(uint64_t seed, uint64_t sub,
@@ -189,9 +199,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     for (int i = threadIdx.x; i < nr; i += blockDim.x) H->rel[i] = a.relc[i];
     __syncthreads();
 
-    const int64_t chain = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const int64_t chain = (int64_t)blockIdx.x;  // (the whole workgroup: one chain)
     if (chain >= a.n_chains) return;
     SpecChain* X = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes + wave * kSpecChainBytes);
+    SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSplit * kSpecChainBytes);
+    const bool w0 = wave == 0, w1 = wave == 1;  // (wave-uniform: whose phases these are)
+    int par = 0;                                  // the batch's SUM buffer
 
     // Frozen flags as a mask, index n frozen (a pick of n is redrawn).
     unsigned int fz = 1u << n;
@@ -217,7 +230,6 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     const Staged<double> RYst{X->RY[g]};
     const Staged<double> Sst{X->S[g]};
     const Staged<float4> CLBst{X->CLB[g]};
-    const Staged<double> SUMst{X->SUM[g]};
     if (r < n) {
         ObjP p;
         p.xf = (float)cx;
@@ -476,34 +488,36 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
         const bool t0 = r < nr && touches(H->rel[r], k1, k2);
         const bool t1 = r + GL < nr && touches(H->rel[r + GL], k1, k2);
-        if (nr + 2 <= GL) {
-            // One atan2 per lane: lane r < nr for relationship r, lanes nr and nr + 1 for the
-            // FocalPoint terms of the moved objects k1 and k2; the cosines go back to them.
-            const int fo = r == nr ? k1 : (r == nr + 1 ? k2 : -1);
-            const bool foc = fo >= 0;
-            const ObjP q = Pg[foc ? fo : 0];
-            double ay = 0.0, ax = 1.0;
-            float ti = 0.0f;
-            if (t0) pw0 = rel_pair(H->rel[r], Pg, ay, ax, ti);
-            if (foc) {
-                ay = (double)(rm.fyf - q.yf);
-                ax = (double)(rm.fxf - q.xf);
-            }
-            float cf = 0.0f;
-            if (__ballot(foc || t0)) {
-                const double at = atan2_ool(ay, ax);
-                if (t0) an0 = rel_angle(H->rel[r], at, ti);
-                if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
-                    const float b = (float)at - q.rotYf;
-                    cf = cos_f32((float)((double)b + kHalfPI));
+        if (w0) {  // (wave 0: the exact FocalPoint and relationship terms)
+            if (nr + 2 <= GL) {
+                // One atan2 per lane: lane r < nr for relationship r, lanes nr and nr + 1 for the
+                // FocalPoint terms of the moved objects k1 and k2; the cosines go back to them.
+                const int fo = r == nr ? k1 : (r == nr + 1 ? k2 : -1);
+                const bool foc = fo >= 0;
+                const ObjP q = Pg[foc ? fo : 0];
+                double ay = 0.0, ax = 1.0;
+                float ti = 0.0f;
+                if (t0) pw0 = rel_pair(H->rel[r], Pg, ay, ax, ti);
+                if (foc) {
+                    ay = (double)(rm.fyf - q.yf);
+                    ax = (double)(rm.fxf - q.xf);
                 }
+                float cf = 0.0f;
+                if (__ballot(foc || t0)) {
+                    const double at = atan2_ool(ay, ax);
+                    if (t0) an0 = rel_angle(H->rel[r], at, ti);
+                    if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
+                        const float b = (float)at - q.rotYf;
+                        cf = cos_f32((float)((double)b + kHalfPI));
+                    }
+                }
+                const float c1 = shfl_f(cf, gbase + nr), c2 = shfl_f(cf, gbase + nr + 1);
+                if (moved) cphs = r == k2 ? c2 : c1;  // (a swap's k2 branch wins, as in the apply)
+            } else if (__ballot(moved || t0 || t1)) {
+                if (moved) cphs = focal_cos(rm, xf, yf, ryf);
+                if (t0) rel_exact(H->rel[r], Pg, pw0, an0);
+                if (t1) rel_exact(H->rel[r + GL], Pg, pw1, an1);
             }
-            const float c1 = shfl_f(cf, gbase + nr), c2 = shfl_f(cf, gbase + nr + 1);
-            if (moved) cphs = r == k2 ? c2 : c1;  // (a swap's k2 branch wins, as in the apply)
-        } else if (__ballot(moved || t0 || t1)) {
-            if (moved) cphs = focal_cos(rm, xf, yf, ryf);
-            if (t0) rel_exact(H->rel[r], Pg, pw0, an0);
-            if (t1) rel_exact(H->rel[r + GL], Pg, pw1, an1);
         }
         SSTAMP(3);
         float4 box = make_float4(0.f, 0.f, 0.f, 0.f), sao = box, sac = box;
@@ -512,30 +526,32 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         if (r < n) {
             const RectShape os = H->objs[r];
             const float area = __int_as_float(os.pad);
-            Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
-            Sst.put(S_VBY + r, (double)area * sy);
-            Sst.put(S_FP + r, -(double)cphs);
+            if (w0) {
+                Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
+                Sst.put(S_VBY + r, (double)area * sy);
+                Sst.put(S_FP + r, -(double)cphs);
+            }
             box = shape_box(os, xf, yf);
             sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
             wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
         }
-        if (r < c) {
+        if (w1 && r < c) {
             const RectShape cs = H->clrs[r];
             const ObjP ps = Pg[cs.pad];
             CLBst.put(r, shape_box(cs, ps.xf, ps.yf));      // Clearance, :414-415
             sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
         }
-        if (r < nr) {
+        if (w0 && r < nr) {
             Sst.put(S_PW + r, -pw0);
             Sst.put(S_ANG + r, -an0);
         }
-        if (r + GL < nr) {
+        if (w0 && r + GL < nr) {
             Sst.put(S_PW + r + GL, -pw1);
             Sst.put(S_ANG + r + GL, -an1);
         }
         // Symmetry row r, Kernel.cu:292-312.
         const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
-        if (r < n) {
+        if (w1 && r < n) {  // (wave 1: symmetry)
             double al = sx * (double)rm.ux;
             al = al + sy * (double)rm.uy;
             const float sd = (float)(2.0 * (rm.along_f - al));
@@ -551,18 +567,25 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
         // (clearances, then objects, :445-480), compacted in the reference's order.
         int ncl = 0, nsa = 0;
-        for (int i = 0; i < c; ++i) {
-            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < n) t4.x = overlap(sv.b[i], box);
-            append4(Sst.at(S_CL), ncl, t4, r < n, r);
+        if (w1) {  // (wave 1: the Clearance / SurfaceArea lists)
+            for (int i = 0; i < c; ++i) {
+                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (r < n) t4.x = overlap(sv.b[i], box);
+                append4(Sst.at(S_CL), ncl, t4, r < n, r);
+            }
+            append4(Sst.at(S_SA), nsa, sac, r < c, r);
+            append4(Sst.at(S_SA), nsa, sao, r < n, r);
         }
-        append4(Sst.at(S_SA), nsa, sac, r < c, r);
-        append4(Sst.at(S_SA), nsa, sao, r < n, r);
         const Published<double> Sv = publish(Sst);
         SSTAMP(5);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
-        // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2).
-        {
+        // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2),
+        // in the wavefront that built it; the workgroup barrier hands them to both. The buffer
+        // alternates by batch: a wavefront starts writing batch t + 1's sums only after the
+        // other has passed batch t + 1's barrier, i.e. finished reading batch t's.
+        const Staged<double> SUMst{SH->SUM[par][g]};
+        const bool mine = w0 ? (r <= 2 || r >= 6) : (r >= 3 && r <= 5);
+        if (mine) {
             int base = S_VBX, len = n;
             bool rnd = true;
             switch (r) {
@@ -583,7 +606,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
             SUMst.put(r, acc);
         }
-        const Published<double> SUMv = publish(SUMst);
+        const Published<double> SUMv = publish_workgroup(SUMst);
+        par ^= 1;
         SSTAMP(6);
         // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547).
         float sc[8];
@@ -632,7 +656,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             const int smode = __builtin_amdgcn_readlane(R.mode, gs << 3);
             const int sk1 = __builtin_amdgcn_readlane(R.k1, gs << 3);
             const int sk2 = __builtin_amdgcn_readlane(R.k2, gs << 3);
-            if (smode == 2 && sk1 >= 0 && lane == 0) {
+            if (smode == 2 && sk1 >= 0 && w0 && lane == 0) {
 #pragma unroll
                 for (int f = 0; f < 3; ++f) {
                     double* row = st + (F_Z + f) * n;
@@ -643,7 +667,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0) {  // [done, kb, off, bmh, gs, committed, cur0] then per group 8 words
+        if (chain == 0 && w0) {  // [done, kb, off, bmh, gs, committed, cur0], per group 8 words
             const unsigned int base = g_spec_dbg_n;
             if (base + 7 + 8 * K < (1u << 16)) {
                 if (lane == 0) {
@@ -682,16 +706,16 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 #endif
     }
 #if MH_STAMPS
-    if (lane == 0)
+    if (w0 && lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
         for (int k = 0; k < 16; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
 #endif
 
-    if (lane < n) {
+    if (w0 && lane < n) {
         st[F_X * n + r] = cx;
         st[F_Y * n + r] = cy;
         st[F_RY * n + r] = cry;
     }
-    if (lane == 0) {
+    if (w0 && lane == 0) {
         ChainMeta m = m0;
         m.accepted = m0.accepted + accepted;
         m.draws = wbase + off;
@@ -730,10 +754,12 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsig
 #endif
 
 size_t spec_lds_bytes(int waves_per_wg) {
-    return (size_t)kSpecHdrBytes + (size_t)waves_per_wg * kSpecChainBytes;
+    return (size_t)kSpecHdrBytes + (size_t)waves_per_wg * kSpecChainBytes + kSpecSharedBytes;
 }
 
-int spec_waves() { return kSpecWaves; }
+// Chains per workgroup (one: its two wavefronts share the chain), and wavefronts per chain.
+int spec_waves() { return 1; }
+int spec_waves_per_chain() { return kSplit; }
 
 // Whether the speculative kernel serves a room: at most GL objects, RMAX relationships.
 bool spec_fits(int n, int c, int r) { return n >= 1 && n <= GL && c <= GL && r <= RMAX; }
@@ -748,7 +774,7 @@ int spec_blocks_per_cu() {
 
 hipError_t launch_spec(const LaunchArgs& a, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
-    const int64_t blocks = (a.n_chains + kSpecWaves - 1) / kSpecWaves;
+    const int64_t blocks = a.n_chains;  // one chain per workgroup
     hipLaunchKernelGGL(mh_spec_kernel, dim3((unsigned)blocks), dim3(64 * kSpecWaves),
                        spec_lds_bytes(kSpecWaves), s, a);
     return hipGetLastError();

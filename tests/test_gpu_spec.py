@@ -46,7 +46,7 @@ def test_spec_chains_match_oracle(mh, orc, hiplib, monkeypatch, kind, n, chains,
     room = _room(mh, kind, n)
     seed = 5150 + n + chains
     with mh.Session(room, chains, seed=seed) as s:
-        assert s.step_kernel() == (64, 4, "speculative")
+        assert s.step_kernel() == (128, 1, "speculative")  # (two wavefronts per chain)
         s.run(steps)
         s.finalize()
         pts, costs = s.download()
