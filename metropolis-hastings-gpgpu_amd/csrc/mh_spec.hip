@@ -4,9 +4,11 @@
 // A chain's draws do not depend on its accept decisions: the object pick redraws on the static
 // frozen flags only (Kernel.cu:598-602), Box-Muller's cached second normal advances with the
 // draws alone, and Accept draws its uniform on every step (:710). So the proposals of steps
-// t .. t+7 are known before any of them is decided. One chain owns a wavefront; its 64 lanes are
-// K = 8 groups of GL = 8 lanes, and group g holds a copy of the current configuration (lane r:
-// object r) and evaluates proposal t + g against it exactly as the reference does (Costs(),
+// t .. t+7 are known before any of them is decided. One chain owns a workgroup of two
+// wavefronts; the 64 lanes of each are K = 8 groups of GL = 8 lanes, and group g holds a copy of
+// the current configuration (lane r: object r) and evaluates proposal t + g against it (wave 0
+// the exact FocalPoint and relationship terms, wave 1 symmetry and the Clearance / SurfaceArea
+// lists, each replaying its own sums) exactly as the reference does (Costs(),
 // Kernel.cu:516-550, every sum in the reference's order). Steps t .. t+g*-1 before the first
 // accepted proposal g* are rejections, which leave the configuration unchanged, so group g*'s
 // evaluation is exactly the sequential chain's: the batch commits steps t .. t+g* and every
