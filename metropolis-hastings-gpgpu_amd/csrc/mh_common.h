@@ -119,6 +119,22 @@ __device__ __forceinline__ Published<A> publish_workgroup(const Staged<A>& a) {
     __syncthreads();
     return Published<A>{a.p};
 }
+template <class A, class B, class C, class D>
+struct Pub4 { Published<A> a; Published<B> b; Published<C> c; Published<D> d; };
+template <class A, class B, class C, class D>
+__device__ __forceinline__ Pub4<A, B, C, D> publish_workgroup(const Staged<A>& a, const Staged<B>& b,
+                                                              const Staged<C>& c, const Staged<D>& d) {
+    __syncthreads();
+    return Pub4<A, B, C, D>{{a.p}, {b.p}, {c.p}, {d.p}};
+}
+// The receiving side of another wavefront's publish_workgroup(a, b, c, d): the same barrier,
+// then the read views.
+template <class A, class B, class C, class D>
+__device__ __forceinline__ Pub4<A, B, C, D> receive_workgroup(const A* a, const B* b, const C* c,
+                                                              const D* d) {
+    __syncthreads();
+    return Pub4<A, B, C, D>{{a}, {b}, {c}, {d}};
+}
 template <class T>
 __device__ __forceinline__ Staged<T> restage(const Published<T>& v) {
     wave_sync();

@@ -68,6 +68,7 @@ struct SpecChain {  // LDS of one chain
     double S[K][S_END];    // each group's ordered-sum streams (this wavefront's)
     float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
     double RY[K][GL];      // each group's double rotY of every object (Symmetry, :305)
+    double XD[K][GL], YD[K][GL];  // each group's double x, y (wave 1's symmetry and boxes)
     ObjP P[K][GL];         // each group's float pose words
     unsigned int wd[128];    // the 128-word window of the Philox stream
     float bs[128], bc[128];  // Box-Muller pairs (word i, word i + 1) of the window
@@ -75,6 +76,7 @@ struct SpecChain {  // LDS of one chain
 
 struct SpecShared {  // LDS of the chain shared by its two wavefronts
     double SUM[2][K][8];  // each group's eight sums (double-buffered by batch parity)
+    int stop;             // wave 0 to wave 1: the chain's steps are done
 };
 
 struct SpecHdr {  // LDS of the workgroup: the room tables
@@ -205,8 +207,76 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     if (chain >= a.n_chains) return;
     SpecChain* X = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes + wave * kSpecChainBytes);
     SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSplit * kSpecChainBytes);
-    const bool w0 = wave == 0, w1 = wave == 1;  // (wave-uniform: whose phases these are)
-    int par = 0;                                  // the batch's SUM buffer
+    const bool w0 = wave == 0;  // (wave-uniform: whose phases these are)
+    int par = 0;                 // the batch's SUM buffer
+    SpecChain* X0 = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes);  // wave 0's (the views)
+
+    if (!w0) {
+        // Wave 1, per batch: wait for wave 0's views of the 8 proposals' configurations, then
+        // the symmetry rows and the Clearance / SurfaceArea lists of every group and their
+        // three ordered sums. It keeps no chain state.
+        const Staged<double> Sst{X->S[g]};
+        const Staged<float4> CLBst{X->CLB[g]};
+#pragma clang loop unroll(disable)
+        for (;;) {
+            const auto pv = receive_workgroup(X0->P[g], X0->RY[g], X0->XD[g], X0->YD[g]);
+            if (SH->stop) break;
+            const ObjP* Pg = pv.a.ptr();
+            const int ro = r < n ? r : 0;
+            const double sx = pv.c[ro], sy = pv.d[ro], sry = pv.b[ro];
+            const float xf = Pg[ro].xf, yf = Pg[ro].yf;
+            float4 box = make_float4(0.f, 0.f, 0.f, 0.f), sao = box, sac = box;
+            bool wild = false;
+            if (r < n) {
+                box = shape_box(H->objs[r], xf, yf);
+                sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
+                wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
+            }
+            if (r < c) {
+                const RectShape cs = H->clrs[r];
+                const ObjP ps = Pg[cs.pad];
+                CLBst.put(r, shape_box(cs, ps.xf, ps.yf));      // Clearance, :414-415
+                sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
+            }
+            // Symmetry row r, Kernel.cu:292-312.
+            const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
+            if (r < n) {
+                double al = sx * (double)rm.ux;
+                al = al + sy * (double)rm.uy;
+                const float sd = (float)(2.0 * (rm.along_f - al));
+                const float rxr = (float)(sx + (double)(sd * rm.ux));
+                const float ryr = (float)(sy + (double)(sd * rm.uy));
+                float rr = (float)(rm.two_focal_rot - sry);
+                if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
+                Sst.put(S_SYM + r, -(double)sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode));
+            }
+            const auto sv = publish(Sst, CLBst);
+            // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
+            // (clearances, then objects, :445-480), compacted in the reference's order.
+            int ncl = 0, nsa = 0;
+            for (int i = 0; i < c; ++i) {
+                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (r < n) t4.x = overlap(sv.b[i], box);
+                append4(Sst.at(S_CL), ncl, t4, r < n, r);
+            }
+            append4(Sst.at(S_SA), nsa, sac, r < c, r);
+            append4(Sst.at(S_SA), nsa, sao, r < n, r);
+            const Published<double> Sv = publish(Sst);
+            // Sums 3 (Symmetry), 4 (Clearance), 5 (SurfaceArea), as in wave 0's replay below.
+            const Staged<double> SUMst{SH->SUM[par][g]};
+            if (r >= 3 && r <= 5) {
+                const int base = r == 3 ? S_SYM : r == 4 ? S_CL : S_SA;
+                const int len = r == 3 ? n : r == 4 ? ncl : nsa;
+                const double* src = Sv.ptr() + base;
+                double acc = 0.0;
+                for (int l = 0; l < len; ++l) acc = (double)(float)(acc + src[l]);
+                SUMst.put(r, acc);
+            }
+            publish_workgroup(SUMst);
+            par ^= 1;
+        }
+        return;
+    }
 
     // Frozen flags as a mask, index n frozen (a pick of n is redrawn).
     unsigned int fz = 1u << n;
@@ -231,7 +301,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     const Staged<ObjP> Pst{X->P[g]};
     const Staged<double> RYst{X->RY[g]};
     const Staged<double> Sst{X->S[g]};
-    const Staged<float4> CLBst{X->CLB[g]};
+    const Staged<double> XDst{X->XD[g]}, YDst{X->YD[g]};
+    const Staged<int> STOP{&SH->stop};
     if (r < n) {
         ObjP p;
         p.xf = (float)cx;
@@ -316,7 +387,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
 #endif
 #pragma clang loop unroll(disable)
-    for (int done = 0; done < a.iterations;) {
+    for (int done = 0;;) {
+        if (done >= a.iterations) {  // (wave 1 leaves its loop at the same barrier)
+            if (lane == 0) STOP.put(0, 1);
+            publish_workgroup(STOP);
+            break;
+        }
         int kb = min(K, a.iterations - done);
         // At most ~5 draws per step (more only for frozen-object redraws, which then draw past
         // the window directly): refill unless 48 remain.
@@ -480,8 +556,11 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             p.pad = 0.0f;
             Pst.put(r, p);
             RYst.put(r, sry);
+            XDst.put(r, sx);
+            YDst.put(r, sy);
         }
-        const auto pv = publish(Pst, RYst);
+        if (lane == 0) STOP.put(0, 0);
+        const auto pv = publish_workgroup(Pst, RYst, XDst, YDst);  // (to wave 1 as well)
         SSTAMP(2);
         const ObjP* Pg = pv.a.ptr();
 
@@ -490,7 +569,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
         const bool t0 = r < nr && touches(H->rel[r], k1, k2);
         const bool t1 = r + GL < nr && touches(H->rel[r + GL], k1, k2);
-        if (w0) {  // (wave 0: the exact FocalPoint and relationship terms)
+        {  // the exact FocalPoint and relationship terms
             if (nr + 2 <= GL) {
                 // One atan2 per lane: lane r < nr for relationship r, lanes nr and nr + 1 for the
                 // FocalPoint terms of the moved objects k1 and k2; the cosines go back to them.
@@ -522,81 +601,35 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
         }
         SSTAMP(3);
-        float4 box = make_float4(0.f, 0.f, 0.f, 0.f), sao = box, sac = box;
-        bool wild = false;
-        float best = 0.0f;
         if (r < n) {
-            const RectShape os = H->objs[r];
-            const float area = __int_as_float(os.pad);
-            if (w0) {
-                Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
-                Sst.put(S_VBY + r, (double)area * sy);
-                Sst.put(S_FP + r, -(double)cphs);
-            }
-            box = shape_box(os, xf, yf);
-            sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
-            wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
+            const float area = __int_as_float(H->objs[r].pad);
+            Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
+            Sst.put(S_VBY + r, (double)area * sy);
+            Sst.put(S_FP + r, -(double)cphs);
         }
-        if (w1 && r < c) {
-            const RectShape cs = H->clrs[r];
-            const ObjP ps = Pg[cs.pad];
-            CLBst.put(r, shape_box(cs, ps.xf, ps.yf));      // Clearance, :414-415
-            sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
-        }
-        if (w0 && r < nr) {
+        if (r < nr) {
             Sst.put(S_PW + r, -pw0);
             Sst.put(S_ANG + r, -an0);
         }
-        if (w0 && r + GL < nr) {
+        if (r + GL < nr) {
             Sst.put(S_PW + r + GL, -pw1);
             Sst.put(S_ANG + r + GL, -an1);
         }
-        // Symmetry row r, Kernel.cu:292-312.
-        const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
-        if (w1 && r < n) {  // (wave 1: symmetry)
-            double al = sx * (double)rm.ux;
-            al = al + sy * (double)rm.uy;
-            const float sd = (float)(2.0 * (rm.along_f - al));
-            const float rxr = (float)(sx + (double)(sd * rm.ux));
-            const float ryr = (float)(sy + (double)(sd * rm.uy));
-            float rr = (float)(rm.two_focal_rot - sry);
-            if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
-            best = sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode);
-            Sst.put(S_SYM + r, -(double)best);
-        }
-        const auto sv = publish(Sst, CLBst);  // (the streams so far are read by the replay)
-        SSTAMP(4);
-        // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
-        // (clearances, then objects, :445-480), compacted in the reference's order.
-        int ncl = 0, nsa = 0;
-        if (w1) {  // (wave 1: the Clearance / SurfaceArea lists)
-            for (int i = 0; i < c; ++i) {
-                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (r < n) t4.x = overlap(sv.b[i], box);
-                append4(Sst.at(S_CL), ncl, t4, r < n, r);
-            }
-            append4(Sst.at(S_SA), nsa, sac, r < c, r);
-            append4(Sst.at(S_SA), nsa, sao, r < n, r);
-        }
         const Published<double> Sv = publish(Sst);
+        SSTAMP(4);
         SSTAMP(5);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
         // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2),
-        // in the wavefront that built it; the workgroup barrier hands them to both. The buffer
-        // alternates by batch: a wavefront starts writing batch t + 1's sums only after the
-        // other has passed batch t + 1's barrier, i.e. finished reading batch t's.
+        // in the wavefront that built it (wave 1: 3, 4, 5); the workgroup barrier hands them to
+        // wave 0. The buffer alternates by batch.
         const Staged<double> SUMst{SH->SUM[par][g]};
-        const bool mine = w0 ? (r <= 2 || r >= 6) : (r >= 3 && r <= 5);
-        if (mine) {
+        if (r <= 2 || r >= 6) {
             int base = S_VBX, len = n;
             bool rnd = true;
             switch (r) {
                 case 0: base = S_VBX; len = n; rnd = true; break;
                 case 1: base = S_VBY; len = n; rnd = true; break;
                 case 2: base = S_FP; len = n; rnd = false; break;
-                case 3: base = S_SYM; len = n; rnd = true; break;
-                case 4: base = S_CL; len = ncl; rnd = true; break;
-                case 5: base = S_SA; len = nsa; rnd = true; break;
                 case 6: base = S_PW; len = nr; rnd = false; break;
                 default: base = S_ANG; len = nr; rnd = false; break;
             }
@@ -658,7 +691,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             const int smode = __builtin_amdgcn_readlane(R.mode, gs << 3);
             const int sk1 = __builtin_amdgcn_readlane(R.k1, gs << 3);
             const int sk2 = __builtin_amdgcn_readlane(R.k2, gs << 3);
-            if (smode == 2 && sk1 >= 0 && w0 && lane == 0) {
+            if (smode == 2 && sk1 >= 0 && lane == 0) {
 #pragma unroll
                 for (int f = 0; f < 3; ++f) {
                     double* row = st + (F_Z + f) * n;
@@ -669,7 +702,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0 && w0) {  // [done, kb, off, bmh, gs, committed, cur0], per group 8 words
+        if (chain == 0) {  // [done, kb, off, bmh, gs, committed, cur0], per group 8 words
             const unsigned int base = g_spec_dbg_n;
             if (base + 7 + 8 * K < (1u << 16)) {
                 if (lane == 0) {
@@ -708,16 +741,16 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 #endif
     }
 #if MH_STAMPS
-    if (w0 && lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
+    if (lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
         for (int k = 0; k < 16; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
 #endif
 
-    if (w0 && lane < n) {
+    if (lane < n) {
         st[F_X * n + r] = cx;
         st[F_Y * n + r] = cy;
         st[F_RY * n + r] = cry;
     }
-    if (w0 && lane == 0) {
+    if (lane == 0) {
         ChainMeta m = m0;
         m.accepted = m0.accepted + accepted;
         m.draws = wbase + off;

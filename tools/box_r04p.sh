@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_spec.py -m gpu -x -v --time
     -p no:cacheprovider -W always::UserWarning > $OUT/pytest_spec.log 2>&1 || { tail -40 $OUT/pytest_spec.log; exit 1; }
 grep -E "passed|failed" $OUT/pytest_spec.log | tail -1
 MH_SPEC=1 timeout -k 10 120 python -u tools/stamps.py 8 1024 2000 > $OUT/stamps_spec.txt 2>&1; rc=$?; cat $OUT/stamps_spec.txt; [ $rc = 0 ] || exit 1
-MH_AB_REPS=2 MH_AB_CFGS="8,1024,2000,4" bash tools/box_abn.sh ${1:-r04p}/ab single main
+MH_AB_REPS=2 MH_AB_CFGS="8,1024,2000,4" bash tools/box_abn.sh ${1:-r04p}/ab split main
