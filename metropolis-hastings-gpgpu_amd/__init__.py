@@ -8,6 +8,5 @@ importlib) rather than a plain import.
 """
 from .abi import (COST_FIELDS, EXPORTS, LIB_PATH, MHError, Room, Session, STRUCT_LAYOUT,  # noqa: F401
                   debug_collectives, debug_math, debug_rng, evaluate_costs, kernel_wrapper,
-                  last_error,
-                  load_library)
+                  last_error, load_library, MH_PROBE_COUNT, probe_width)
 from .rooms import clone_cfg, main_fixture, synthetic_room  # noqa: F401

@@ -329,9 +329,25 @@ def debug_rng(seed: int, subsequence: int, n: int, rng: int = MH_RNG_PHILOX):
             np.frombuffer(bytes(g), dtype=np.float32).copy())
 
 
-def debug_math(fn: int, start: int, count: int, width: int) -> np.ndarray:
+# doubles each probe writes per argument (mh_math.h mh_probe_width: the sincos probes 2)
+MH_PROBE_COUNT = 11
+_PROBE_WIDTH = {1: 2, 4: 2}  # MH_PROBE_BM_SINCOS, MH_PROBE_XW_SINCOS
+
+
+def probe_width(fn: int) -> int:
+    return _PROBE_WIDTH.get(fn, 1)
+
+
+def debug_math(fn: int, start: int, count: int, width: int | None = None) -> np.ndarray:
     """mh_debug_math: the shared transcendentals' probe `fn` evaluated on the device, float64
-    [count, width] (diagnostic; tests/test_gpu_math.py)."""
+    [count, width] (diagnostic; tests/test_gpu_math.py). The C side writes probe_width(fn)
+    doubles per argument, so the buffer is sized from `fn`; a `width` that disagrees is an
+    error, not a short buffer."""
+    if not 0 <= fn < MH_PROBE_COUNT:
+        raise ValueError(f"unknown probe {fn}")
+    if width is not None and width != probe_width(fn):
+        raise ValueError(f"probe {fn} writes {probe_width(fn)} values per argument, not {width}")
+    width = probe_width(fn)
     lib = load_library()
     out = np.empty((count, width), dtype=np.float64)
     if lib.mh_debug_math(fn, C.c_uint64(start), C.c_uint64(count), out.ctypes.data) != 0:

@@ -562,7 +562,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     }
 #pragma unroll 2
     for (int j = 0; j < ((MH_ABLATE & 1) ? 0 : n); ++j) {
-        const float4 q = *reinterpret_cast<const float4*>(&ch.P[j]);
+        const float4 q = objp_f4(ch.P[j]);
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
             const float v = sym_val_fast(q, rxs[m], rys[m], rrs[m]);
@@ -610,7 +610,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
 #pragma unroll
             for (int m = 0; m < NPL; ++m) {
                 if (amb[m]) {
-                    const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rxs[m],
+                    const float v = sym_val_fast(objp_f4(q), rxs[m],
                                                  rys[m], rrs[m]);
                     if (!(v < m1[m] - thr[m])) {
                         const float e = sym_val_exact(q.xf, q.yf, ryj, rxs[m], rys[m],
@@ -663,8 +663,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     bool need[NPL];
     unsigned pend[NPL];
     float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
-    if (ka >= 0) qa = *reinterpret_cast<const float4*>(&ch.P[ka]);
-    if (kb >= 0) qb = *reinterpret_cast<const float4*>(&ch.P[kb]);
+    if (ka >= 0) qa = objp_f4(ch.P[ka]);
+    if (kb >= 0) qb = objp_f4(ch.P[kb]);
     // the changed columns' rotY, from their owner lanes (ka, kb are group-uniform)
     const double rya = pose_ry<L, NPL>(op, ka < 0 ? 0 : ka, gbase);
     const double ryb = pose_ry<L, NPL>(op, kb < 0 ? 0 : kb, gbase);
@@ -758,7 +758,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const int j = q * L + r;
             if (j < n) {
                 const float v =
-                    sym_val_fast(*reinterpret_cast<const float4*>(&ch.P[j]), rx, ry, rr);
+                    sym_val_fast(objp_f4(ch.P[j]), rx, ry, rr);
                 t2 = __builtin_amdgcn_fmed3f(t1, t2, v);
                 const bool up = v > t1;
                 t1 = up ? v : t1;
@@ -779,7 +779,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                 const int j = q * L + r;
                 if (j >= n) break;
                 const ObjP p = ch.P[j];
-                const float v = sym_val_fast(*reinterpret_cast<const float4*>(&p), rx, ry, rr);
+                const float v = sym_val_fast(objp_f4(p), rx, ry, rr);
                 if (!(v < ld.m - thr)) {
                     const float e = sym_val_exact(p.xf, p.yf, op.ry[q], rx, ry, (double)rr);
                     if (e > bv) {
@@ -1175,8 +1175,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         for (int l0 = 0; l0 < steps; l0 += 4) {
             // every stream holds doubles; a lane past its end reads four zeros
             const double* src = l0 < len ? dsrc + l0 : ch.zero4;
-            const double2 a0 = *reinterpret_cast<const double2*>(src);
-            const double2 a1 = *reinterpret_cast<const double2*>(src + 2);
+            const double2 a0 = load16<double2>(src);
+            const double2 a1 = load16<double2>(src + 2);
             const double v[4] = {a0.x, a0.y, a1.x, a1.y};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1187,8 +1187,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         if (k == 4 && len > steps) {
             float a32 = (float)accf;
             for (int l0 = steps; l0 < len; l0 += 4) {
-                const double2 a0 = *reinterpret_cast<const double2*>(dsrc + l0);
-                const double2 a1 = *reinterpret_cast<const double2*>(dsrc + l0 + 2);
+                const double2 a0 = load16<double2>(dsrc + l0);
+                const double2 a1 = load16<double2>(dsrc + l0 + 2);
                 a32 = a32 + (float)a0.x;
                 a32 = a32 + (float)a0.y;
                 a32 = a32 + (float)a1.x;

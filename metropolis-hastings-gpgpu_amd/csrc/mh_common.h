@@ -57,11 +57,25 @@ __device__ __forceinline__ bool mh_check_fail(unsigned site, unsigned v0, unsign
 
 namespace mh {
 
-struct ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
+struct alignas(16) ObjP {  // per-object pose words read by the O(N^2) symmetry scan: one ds_read_b128
     float xf, yf;  // (float)x, (float)y -- every O(N^2) use of x, y is through float args
     float rotYf;   // (float)rotY
     float pad;
 };
+
+// 16-byte value loads. Memory is only ever accessed through its own type: a vector view of an
+// ObjP or of a double / float stream is a byte copy into a local (one ds_read_b128 for 16-byte
+// aligned LDS), never a dereference of a pointer cast to another object type, which strict
+// aliasing lets the optimiser reorder against the real type's stores (tests/test_abi.py
+// test_no_type_punning keeps it that way).
+template <class V, class T>
+__device__ __forceinline__ V load16(const T* p) {
+    static_assert(sizeof(V) == 16, "16-byte loads only");
+    V v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 16), 16);
+    return v;
+}
+__device__ __forceinline__ float4 objp_f4(const ObjP& p) { return load16<float4>(&p); }
 
 // ---- wave-level helpers -----------------------------------------------------------------
 

@@ -772,11 +772,14 @@ __device__ __forceinline__ void save_best_delta(const DeltaPtrs& ch, const Own<S
 // entries up to round4(to) are zero (x + 0 == x).
 // The next four terms are loaded before the current four are added, so the LDS latency
 // overlaps the dependent adds (these walks run ~1,000 terms at N = 256 on few waves per SIMD).
-__device__ __forceinline__ float list_walk(const float* fs, int from, int to, float a) {
+// (`fs`: a float list, or the replay's byte view of one)
+template <class T>
+__device__ __forceinline__ float list_walk(const T* fs, int from, int to, float a) {
     if (from >= to) return a;
-    float4 q = *reinterpret_cast<const float4*>(fs + from);
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(fs);
+    float4 q = load16<float4>(b + 4 * from);
     for (int l = from; l < to; l += 4) {
-        const float4 nq = (l + 4 < to) ? *reinterpret_cast<const float4*>(fs + l + 4) : q;
+        const float4 nq = (l + 4 < to) ? load16<float4>(b + 4 * (l + 4)) : q;
         a = a + q.x;
         a = a + q.y;
         a = a + q.z;
@@ -799,19 +802,21 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     const int k = r;
     const float* ms = ch.ONES;
     const double* ds = ch.ZERO;
-    const float* fs = reinterpret_cast<const float*>(ch.ZERO);
+    // the float streams as bytes: a lane past its stream's end reads the zero doubles' bytes,
+    // so its float terms are value copies (load16), never float lvalues on double storage
+    const unsigned char* fs = reinterpret_cast<const unsigned char*>(ch.ZERO);
     int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
         ds = k == 0 ? ch.X : ch.Y;
     } else if (k == 2) {
-        fs = ch.CPH;
+        fs = reinterpret_cast<const unsigned char*>(ch.CPH);
     } else if (k == 3) {
-        fs = ch.NMX;
+        fs = reinterpret_cast<const unsigned char*>(ch.NMX);
     } else if (k == 4) {
-        fs = ch.LCL;
+        fs = reinterpret_cast<const unsigned char*>(ch.LCL);
     } else if (k == 5) {
-        fs = ch.LSA;  // (its capacity may be below NP: the stream ends at the zero-filled end)
+        fs = reinterpret_cast<const unsigned char*>(ch.LSA);  // (its capacity may be below NP: the stream ends at the zero-filled end)
         lim = (min(cnt_sa, ch.cap_sa) + 3) & ~3;
     } else if (k == 6) {
         ds = ch.RPW;
@@ -825,13 +830,17 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
         const bool in = l0 < lim;
         const float* msl = in ? ms : ch.ONES;
         const double* dsl = in ? ds : ch.ZERO;
-        const float* fsl = in ? fs : reinterpret_cast<const float*>(ch.ZERO);
+        const unsigned char* fsl = in ? fs : reinterpret_cast<const unsigned char*>(ch.ZERO);
+        float fv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)  // (4-byte value loads: the compiler pairs them, ds_read2_b32)
+            __builtin_memcpy(&fv[u], __builtin_assume_aligned(fsl + 4 * (l0 + u), 4), 4);
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             // one rounding either way: rn(m * d) where f = 0 (VisualBalance: m = area) and
             // rn(d + f) where m = 1 (every other sum), so the fused form is the two-step one
-            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fsl[l0 + u]);
+            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fv[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];

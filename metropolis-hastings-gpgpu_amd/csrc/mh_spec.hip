@@ -139,7 +139,7 @@ __device__ __forceinline__ float sym_row(const ObjP* P, const double* RY, int n,
     float m1 = -INFINITY, m2 = -INFINITY;
     int j1 = -1;
     for (int j = 0; j < n; ++j) {
-        const float4 q = *reinterpret_cast<const float4*>(&P[j]);
+        const float4 q = objp_f4(P[j]);
         const float v = sym_val_fast(q, rx, ry, rr);
         m2 = __builtin_amdgcn_fmed3f(m1, m2, v);
         const bool up = v > m1;
@@ -155,7 +155,7 @@ __device__ __forceinline__ float sym_row(const ObjP* P, const double* RY, int n,
         const float thr = (exact_mode || j1 < 0) ? INFINITY : 2.0f * sym_err(fabsf(m1) + 1.0f, rr);
         for (int j = 0; j < n; ++j) {
             const ObjP q = P[j];
-            const float v = sym_val_fast(*reinterpret_cast<const float4*>(&q), rx, ry, rr);
+            const float v = sym_val_fast(objp_f4(q), rx, ry, rr);
             if (!(v < m1 - thr)) best = fmaxf(best, sym_val_exact(q.xf, q.yf, RY[j], rx, ry, (double)rr));
         }
     }

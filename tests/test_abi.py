@@ -89,6 +89,44 @@ def test_step_kernels_make_no_calls(mh, tmp_path):
     assert helpers <= allowed, sorted(helpers - allowed)
 
 
+_BYTE_TYPES = {"char", "unsigned char", "signed char", "uint8_t", "std::byte", "void"}
+# the LDS carve-up: `lds` is the extern __shared__ unsigned char array and `base` a chain's byte
+# pointer into it; a typed array placed there is only ever accessed through its own type
+_BYTE_POINTERS = {"lds", "base", "s->d_meta"}
+
+
+def test_no_type_punning():
+    """No memory is read or written through a pointer cast between unrelated object types
+    (strict aliasing; the class of undefined behaviour DESIGN.md "The counting-build fault" blames
+    for round 3's wrong code out of line). Allowed: casts to byte pointers, and casts from the LDS
+    byte pointers that place a typed array. Vector views of other types go through load16()
+    (mh_common.h), a value copy."""
+    csrc = ROOT / "metropolis-hastings-gpgpu_amd" / "csrc"
+    text = {f.name: f.read_text() for f in sorted(csrc.iterdir())
+            if f.suffix in (".hip", ".h", ".cpp")}
+    text["mh_kernel.h"] = HEADER.read_text()
+    cast = re.compile(r"reinterpret_cast<\s*(?:const\s+)?([\w:\s]+?)\s*(?:const\s*)?\*\s*>\s*\(\s*"
+                      r"(&?[\w\->\.]+)")
+    bad = []
+    for name, src in text.items():
+        for m in cast.finditer(src):
+            target, operand = m.group(1).strip(), m.group(2)
+            if target in _BYTE_TYPES or operand in _BYTE_POINTERS:
+                continue
+            bad.append(f"{name}:{src.count(chr(10), 0, m.start()) + 1}: {m.group(0)}")
+        # C-style pointer casts and unions are not used for punning either
+        for m in re.finditer(r"\(\s*(?:const\s+)?(?:float|double|u?int\d*_t|int|unsigned|u?int[24]|"
+                             r"float[24]|double2)\s*\*\s*\)\s*&", src):
+            bad.append(f"{name}:{src.count(chr(10), 0, m.start()) + 1}: {m.group(0)}")
+        for m in re.finditer(r"\bunion\b", src):
+            bad.append(f"{name}:{src.count(chr(10), 0, m.start()) + 1}: union")
+    assert not bad, "type punning:\n" + "\n".join(bad)
+    # the byte pointers really are byte pointers
+    assert "extern __shared__ __attribute__((aligned(16))) unsigned char lds[];" in text["mh_chain.hip"]
+    assert "unsigned char* base = lds" in text["mh_chain.hip"]
+    assert "unsigned char* base = lds" in text["mh_delta.hip"]
+
+
 @pytest.mark.parametrize("lang,compiler", [("c", "gcc"), ("c++", "g++")])
 def test_header_compiles_and_links(mh, tmp_path, lang, compiler):
     src = tmp_path / ("t.c" if lang == "c" else "t.cpp")
@@ -151,3 +189,15 @@ def test_null_arguments(mh, hiplib):
     assert "srf" in mh.last_error(hiplib)
     assert not hiplib.KernelWrapper(*room.args(), None)
     hiplib.KernelFreeResult(None)
+
+
+def test_debug_math_buffer_sized_from_probe(mh, orc):
+    """mh_debug_math writes mh_probe_width(fn) doubles per argument: the wrapper sizes its buffer
+    from the probe id (the oracle's table agrees) and rejects a width that disagrees before any
+    call."""
+    for fn in range(mh.MH_PROBE_COUNT):
+        assert mh.probe_width(fn) == orc.probe_width(fn), fn
+    with pytest.raises(ValueError):
+        mh.debug_math(1, 0, 4, 1)  # a sincos probe writes 2
+    with pytest.raises(ValueError):
+        mh.debug_math(mh.MH_PROBE_COUNT, 0, 4)

@@ -172,6 +172,31 @@ def test_config4_rank7_shard(mh, orc, hiplib):
     _check_summary("config 4 rank-7 shard", summ, costs, offset=offset)
 
 
+@pytest.mark.parametrize("name,n,chains,offset", [
+    ("config 3", 64, 65536, 0),
+    ("config 4 rank-7 shard", 64, 65536, 7 * 65536),
+    ("config 5", 256, 32768, 0)])
+def test_every_chain_short(mh, orc, hiplib, name, n, chains, offset):
+    """Every chain of a config's full population, at 20 steps: each workgroup slot, wavefront
+    and global id -> Philox subsequence mapping of the launch (one chain per block id,
+    Kernel.cu:950) compared bit for bit with the oracle, not a sample. (The long runs above
+    compare sampled chains; this covers the whole population at the cost of length.)"""
+    room = mh.synthetic_room(n)
+    steps, seed = 20, 42
+    with mh.Session(room, chains, seed=seed, chain_offset=offset) as s:
+        s.run(steps)
+        s.finalize()
+        pts, costs = s.download()
+        summ = s.summary()
+    ref_pts, ref_costs, ref_acc = orc.run_chains(room, chains, steps, seed, chain_begin=offset,
+                                                 threads=HOST_THREADS)
+    check_chains(f"{name} (N={n}, all {chains} chains x {steps} steps"
+                 + (f", global ids from {offset}" if offset else "") + ")",
+                 pts, costs, ref_pts, ref_costs, ids=offset + np.arange(chains), report=True)
+    assert summ.accepted == int(np.asarray(ref_acc).sum())
+    _check_summary(f"{name} ({steps} steps)", summ, costs, offset=offset)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

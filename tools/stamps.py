@@ -13,10 +13,7 @@ sys.path.insert(0, str(ROOT))
 os.environ.setdefault("MH_LIB", str(ROOT / "ablate" / "libmhgpu_stamps.so"))
 import __graft_entry__ as graft  # noqa: E402
 
-DELTA_SPEC_PHASES = ["refill", "scan: group records", "apply + views", "per-object exact terms",
-               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
-               "scan: lane parse", "scan: walk", "", ""]
-PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
+DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
 SPEC_PHASES = ["refill", "scan: group records", "apply + views", "per-object exact terms",
                "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
