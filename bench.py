@@ -264,11 +264,26 @@ def main() -> int:
                                       s.accepted), dtype=torch.float64,
                        device=cdev)
     times = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=cdev)
+    # this rank's identity and timing, so a multi-rank line shows which GPU each rank drove
+    props = torch.cuda.get_device_properties(device)
+    pci = [getattr(props, k, -1) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    me = torch.tensor([rank, device, *pci, wall, kernel_ms, offset, count], dtype=torch.float64,
+                      device=cdev)
+    ranks = None
     if world > 1:
         gathered = [torch.empty_like(rec) for _ in range(world)]
         dist.all_gather(gathered, rec)
+        everyone = [torch.empty_like(me) for _ in range(world)]
+        dist.all_gather(everyone, me)
         dist.all_reduce(times, op=dist.ReduceOp.MAX)
         recs = torch.stack(gathered).cpu()
+        ranks = [dict(zip(("rank", "device", "pci_domain", "pci_bus", "pci_device", "wall_s",
+                           "kernel_ms", "chain_offset", "chains"), map(float, e.cpu().tolist())))
+                 for e in everyone]
+        for d in ranks:
+            for k in ("rank", "device", "pci_domain", "pci_bus", "pci_device", "chain_offset",
+                      "chains"):
+                d[k] = int(d[k])
     else:
         recs = rec.unsqueeze(0).cpu()
     wall, kernel_ms = float(times[0]), float(times[1])
@@ -355,6 +370,15 @@ def main() -> int:
                 "pmc_status": pmc_status,
             },
             "cpu_baseline": cpu,
+            # world > 1: what the collective saw (backend, communicator size) and every rank's
+            # device, PCI address and timing; distinct PCI addresses = distinct GPUs
+            "distributed": ({
+                "backend": dist.get_backend(),
+                "world_size": dist.get_world_size(),
+                "distinct_gpus": len({(d["pci_domain"], d["pci_bus"], d["pci_device"])
+                                      for d in ranks}),
+                "ranks": ranks,
+            } if world > 1 else None),
             "e2e_chain_steps_per_s": e2e["chain_steps_per_s"] if e2e else None,
             "e2e": e2e,
         }

@@ -21,6 +21,17 @@
  *
  * Functions: mh_log, mh_exp, mh_sincos / mh_sin / mh_cos (any finite double: Cody-Waite
  * reduction below 2^20 pi/2, Payne-Hanek with a 1280-bit table of 2/pi above), mh_atan2.
+ *
+ * fdlibm's notice, preserved as its licence asks (the constants, polynomial coefficients and
+ * algorithms below derive from e_log.c, e_exp.c, k_sin.c, k_cos.c, e_rem_pio2.c, k_rem_pio2.c,
+ * s_atan.c and e_atan2.c):
+ *
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this
+ *   software is freely granted, provided that this notice
+ *   is preserved.
  */
 #ifndef MH_MATH_H_
 #define MH_MATH_H_

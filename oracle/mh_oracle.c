@@ -21,7 +21,7 @@
  * Defined semantics where the reference is ill-defined:
  *   - one proposer per chain and a full state copy each step (the reference races when
  *     blockDim.x > 1, Kernel.cu:798, and copies with a broken stride, :733-734);
- *   - a drawn index == nObjs (u == 1.0f with nObjs >= 64, :566-574) counts as frozen and is
+ *   - a drawn index == nObjs (u == 1.0f with nObjs >= 33, :566-574) counts as frozen and is
  *     redrawn; all-frozen rooms are a validation error instead of an endless loop (:600-602);
  *   - the chain's result is its final current state plus that state's cost components.
  */

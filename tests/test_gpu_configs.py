@@ -10,6 +10,8 @@ the reference edges that short runs do not reach -- each chain bit for bit again
 * config 4: one rank's shard (global ids 7*65,536 ...), the 2-rank bench.py launcher path, and
   KernelWrapper's in-process $MH_DEVICES sharding (unmeasured on 8 GPUs: the driver runs those);
 * config 5: 64 chains sampled out of a 32,768-chain, 10k-step session of the 256-object room;
+* every chain of configs 3, 4 (rank 7's shard) and 5 at 20 steps: the whole population's
+  workgroup slots and global id -> Philox subsequence mapping, not a sample;
 * the index-n pick (u == 1.0f, Kernel.cu:566-574,598-602) on every RNG path, from a searched
   fixture (tests/golden/find_index_n.py);
 * KernelWrapper's $MH_SEED against KernelWrapperSeeded (Kernel.cu:873,943);
@@ -188,8 +190,9 @@ def test_every_chain_short(mh, orc, hiplib, name, n, chains, offset):
         s.finalize()
         pts, costs = s.download()
         summ = s.summary()
-    ref_pts, ref_costs, ref_acc = orc.run_chains(room, chains, steps, seed, chain_begin=offset,
-                                                 threads=HOST_THREADS)
+    with _fast_oracle(orc):
+        ref_pts, ref_costs, ref_acc = orc.run_chains(room, chains, steps, seed,
+                                                     chain_begin=offset, threads=HOST_THREADS)
     check_chains(f"{name} (N={n}, all {chains} chains x {steps} steps"
                  + (f", global ids from {offset}" if offset else "") + ")",
                  pts, costs, ref_pts, ref_costs, ids=offset + np.arange(chains), report=True)
@@ -229,6 +232,12 @@ def test_config4_two_rank_bench_equals_one_session(mh, hiplib, tmp_path):
     assert rec["best_final_cost"] == float(summ.best_total)
     assert rec["accepted"] == summ.accepted
     assert rec["mean_final_cost"] == pytest.approx(summ.sum_total / (2 * per), rel=1e-12)
+    # the line names what the collective saw: backend, communicator size, each rank's device
+    dist_rec = rec["distributed"]
+    assert dist_rec["backend"] == "gloo" and dist_rec["world_size"] == 2
+    assert [d["rank"] for d in dist_rec["ranks"]] == [0, 1]
+    assert [d["chain_offset"] for d in dist_rec["ranks"]] == [0, per]
+    assert dist_rec["distinct_gpus"] == 1  # (two ranks share this box's one GPU)
 
 
 def test_kernelwrapper_mh_devices_sharding(mh, hiplib, monkeypatch):
@@ -281,14 +290,17 @@ STEP_PATHS = [  # (name, env): every RNG path a chain can take (speculative: N <
 ]
 
 
-@pytest.mark.parametrize("path", STEP_PATHS, ids=[p[0] for p in STEP_PATHS])
+# The index-n pick needs nObjs >= 33 (tests/test_oracle.py test_index_n_needs_33_objects), and
+# the speculative kernel serves rooms of at most 8 objects, so it never meets one.
+INDEX_N_PATHS = [p for p in STEP_PATHS if p[0] != "speculative"]
+
+
+@pytest.mark.parametrize("path", INDEX_N_PATHS, ids=[p[0] for p in INDEX_N_PATHS])
 @pytest.mark.parametrize("case", GOLDEN["index_n"], ids=lambda c: f"chain{c['chain']}")
 def test_index_n_pick_redrawn(mh, orc, hiplib, monkeypatch, case, path):
     """A chain whose pick draws u == 1.0f: generateRandomIntInRange(63, 0) gives 64 = nObjs
     (Kernel.cu:566-574), redrawn like a frozen object. The oracle must see the event; the device
-    must reproduce the chain bit for bit on every step kernel and RNG path."""
-    if path[0] == "speculative" and case["n"] > 8:
-        pytest.skip("the speculative kernel serves rooms of at most 8 objects")
+    must reproduce the chain bit for bit on every step kernel and RNG path that serves N >= 33."""
     for k, v in path[1].items():
         monkeypatch.setenv(k, v)
     room = mh.synthetic_room(case["n"])

@@ -1,6 +1,7 @@
-"""The speculative step kernel (mh_spec.hip: rooms of at most 8 objects with few chains; each
-wavefront evaluates 8 consecutive proposals of one chain and commits up to the first accepted
-one) against the oracle's sequential chain, bit for bit: every chain's final poses and costs."""
+"""The speculative step kernel (mh_spec.hip: rooms of at most 8 objects with few chains; a batch
+evaluates the 8 nodes of a tree of accept / reject histories of one chain and commits the
+realised path) against the oracle's sequential chain, bit for bit: every chain's final poses and
+costs, over rooms whose acceptance rates grow different trees."""
 import numpy as np
 import pytest
 
@@ -21,6 +22,11 @@ def _room(mh, kind, n):
         for k in range(room.srf.nRelationships):
             room.rsa[k].angleMin = 7 * PI / 4
             room.rsa[k].angleMax = PI / 4
+    if kind in ("flat", "steep"):  # acceptance near 1 / low: the tree grows deep accept / reject
+        scale = 0.0 if kind == "flat" else 40.0  # paths (spec_tree adapts every 32 batches)
+        for w in ("WeightFocalPoint", "WeightPairWise", "WeightVisualBalance", "WeightSymmetry",
+                  "WeightClearance", "WeightSurfaceArea"):
+            setattr(room.srf, w, getattr(room.srf, w) * scale)
     if kind == "cramped":  # objects piled up: many Clearance / SurfaceArea terms, symmetry ties
         for j in range(n):
             room.cfg[j].x = 0.3 * (j % 3)
@@ -40,6 +46,9 @@ def _room(mh, kind, n):
     ("wrap", 8, 128, 600),
     ("cramped", 8, 128, 600),
     ("frozen", 3, 64, 400),
+    ("flat", 8, 128, 1500),   # every proposal accepted (u < 1): all-accept trees
+    ("steep", 8, 128, 1500),  # few accepted: near-linear trees
+    ("flat", 2, 64, 1200),
 ])
 def test_spec_chains_match_oracle(mh, orc, hiplib, monkeypatch, kind, n, chains, steps):
     monkeypatch.setenv("MH_SPEC", "1")
@@ -51,6 +60,9 @@ def test_spec_chains_match_oracle(mh, orc, hiplib, monkeypatch, kind, n, chains,
         s.finalize()
         pts, costs = s.download()
         cur = s.current_costs()
+        acc = s.summary().accepted
+    if kind == "flat":
+        assert acc > 0.99 * chains * steps
     ref_pts, ref_costs, _ = orc.run_chains(room, chains, steps, seed, threads=8)
     check_chains(f"speculative {kind} N={n}", pts, costs, ref_pts, ref_costs, report=True)
     # the costs each chain carries equal the final pass's, OffLimits aside

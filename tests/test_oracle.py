@@ -69,7 +69,7 @@ def test_uniform_conversion(orc):
 
 
 def test_index_n_is_redrawn(mh, orc):
-    """generateRandomIntInRange(N-1, 0) with u == 1.0f returns N for N >= 64 (Kernel.cu:571);
+    """generateRandomIntInRange(N-1, 0) with u == 1.0f returns N for N >= 33 (Kernel.cu:571);
     the defined chain treats index N as frozen and redraws."""
     lib = orc.load()
     r = _rng_with_words(orc, [0xFFFFFFFF] * 4)
@@ -84,6 +84,17 @@ def test_index_n_is_redrawn(mh, orc):
     r = _rng_with_words(orc, [0x18000000, 0x28000000, 0, 0])  # picks 1 (frozen), then 2
     k = lib.orc_pick_object(C.cast(frozen.cfg, C.c_void_p), 16, C.byref(r))
     assert frozen.cfg[1].frozen and k == 2
+
+
+def test_index_n_needs_33_objects(orc):
+    """The index-n pick exists only from 33 objects up: u == 1.0f (the largest uniform; the
+    result grows with u) gives generateRandomIntInRange(N-1, 0) = N - 1 for every N <= 32 and N
+    for N = 33..256, where N - 1 + 0.999999 rounds up to the float N (Kernel.cu:566-574). So the
+    speculative kernel (N <= 8) never meets it."""
+    lib = orc.load()
+    for n in range(1, 257):
+        r = _rng_with_words(orc, [0xFFFFFFFF] * 4)
+        assert lib.orc_rand_int(C.byref(r), n - 1, 0) == (n if n >= 33 else n - 1), n
 
 
 def test_swap_with_itself_rounds_to_float(mh, orc):
