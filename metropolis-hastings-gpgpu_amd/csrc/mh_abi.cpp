@@ -17,6 +17,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -394,6 +395,16 @@ struct mh_session {
     point* d_pts = nullptr;
     resultCosts* d_costs = nullptr;
     mh_summary* d_summary = nullptr;
+    // Element capacities of the buffers above: a pooled session (KernelWrapper's cache) keeps
+    // its buffers across calls and grows one only when a call needs more.
+    size_t cap_obj = 0, cap_clr = 0, cap_rel = 0, cap_cfg0 = 0, cap_st = 0, cap_best = 0,
+           cap_xw = 0, cap_ladder = 0, cap_perm = 0, cap_meta = 0, cap_pts = 0, cap_costs = 0,
+           cap_summary = 0;
+    // The geometry's inputs (choose_geometry runs only when they change)
+    bool geo_valid = false;
+    int geo_n = -1, geo_c = -1, geo_r = -1;
+    int64_t geo_chains = -1;
+    bool geo_plain = false;
 
     static float bound_slack() {
         const char* e = getenv("MH_BOUND_SLACK");
@@ -457,9 +468,24 @@ void free_session(mh_session* s) {
     delete s;
 }
 
+// A device buffer of at least `count` elements: the one held if it is large enough, else a new
+// one (a pooled session's earlier work on it is complete: it was downloaded and synchronised
+// before the session went back to the pool).
 template <class T>
-bool upload(T** dst, const std::vector<T>& src, hipStream_t st) {
-    MH_TRY_HIP(hipMalloc((void**)dst, sizeof(T) * src.size()));
+bool ensure(T** p, size_t& cap, size_t count) {
+    if (count == 0) count = 1;
+    if (*p && cap >= count) return true;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    MH_TRY_HIP(hipMalloc((void**)p, sizeof(T) * count));
+    cap = count;
+    return true;
+}
+
+template <class T>
+bool upload(T** dst, size_t& cap, const std::vector<T>& src, hipStream_t st) {
+    if (!ensure(dst, cap, src.size())) return false;
     MH_TRY_HIP(hipMemcpyAsync(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice, st));
     return true;
 }
@@ -480,41 +506,52 @@ bool record_done(mh_session* s, hipStream_t st) {
     return true;
 }
 
+// Sets a session up for its room, chains and options. A pooled session (KernelWrapper's cache)
+// comes here again for every call: its stream and event are kept, its buffers grow only when
+// too small, and the geometry is chosen again only for another room shape or chain count.
 bool session_init(mh_session* s) {
     MH_TRY_HIP(hipSetDevice(s->device));
-    MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    MH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    if (!s->stream) MH_TRY_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!s->done) MH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
     s->last = s->stream;
+    s->steps_done = 0;
     const bool plain = s->track == mh::TRACK_OFF && s->n_temps <= 1 && s->rng == mh::RNG_PHILOX;
-    if (!choose_geometry(s->room.rm.n, s->room.rm.c, s->room.rm.r, s->device, s->n_chains, plain,
-                         s->geo))
-        return false;
-    if (!upload(&s->d_obj, s->room.obj, s->stream)) return false;
-    if (!upload(&s->d_clr, s->room.clr, s->stream)) return false;
-    if (!upload(&s->d_rel, s->room.rel, s->stream)) return false;
-    if (!upload(&s->d_cfg0, s->room.cfg0, s->stream)) return false;
+    const int rn = s->room.rm.n, rc = s->room.rm.c, rr = s->room.rm.r;
+    if (!(s->geo_valid && s->geo_n == rn && s->geo_c == rc && s->geo_r == rr &&
+          s->geo_chains == s->n_chains && s->geo_plain == plain)) {
+        s->geo_valid = false;
+        if (!choose_geometry(rn, rc, rr, s->device, s->n_chains, plain, s->geo)) return false;
+        s->geo_valid = true;
+        s->geo_n = rn;
+        s->geo_c = rc;
+        s->geo_r = rr;
+        s->geo_chains = s->n_chains;
+        s->geo_plain = plain;
+    }
+    if (!upload(&s->d_obj, s->cap_obj, s->room.obj, s->stream)) return false;
+    if (!upload(&s->d_clr, s->cap_clr, s->room.clr, s->stream)) return false;
+    if (!upload(&s->d_rel, s->cap_rel, s->room.rel, s->stream)) return false;
+    if (!upload(&s->d_cfg0, s->cap_cfg0, s->room.cfg0, s->stream)) return false;
     const int64_t nc = s->n_chains > 0 ? s->n_chains : 1;
     const size_t n = (size_t)s->room.rm.n;
-    MH_TRY_HIP(hipMalloc((void**)&s->d_st, sizeof(double) * mh::F_COUNT * n * nc));
-    if (s->track != mh::TRACK_OFF)
-        MH_TRY_HIP(hipMalloc((void**)&s->d_best, sizeof(double) * mh::F_COUNT * n * nc));
+    if (!ensure(&s->d_st, s->cap_st, (size_t)mh::F_COUNT * n * nc)) return false;
+    if (s->track != mh::TRACK_OFF && !ensure(&s->d_best, s->cap_best, (size_t)mh::F_COUNT * n * nc))
+        return false;
     if (s->n_temps > 1) {
-        MH_TRY_HIP(hipMalloc((void**)&s->d_ladder, sizeof(double) * s->n_temps));
-        MH_TRY_HIP(hipMemcpyAsync(s->d_ladder, s->ladder.data(), sizeof(double) * s->n_temps,
-                                  hipMemcpyHostToDevice, s->stream));
+        if (!upload(&s->d_ladder, s->cap_ladder, s->ladder, s->stream)) return false;
         std::vector<int> perm((size_t)nc);
         for (int64_t i = 0; i < (int64_t)perm.size(); ++i) perm[(size_t)i] = (int)(i % s->n_temps);
-        MH_TRY_HIP(hipMalloc((void**)&s->d_perm, sizeof(int) * perm.size()));
+        if (!ensure(&s->d_perm, s->cap_perm, perm.size())) return false;
         MH_TRY_HIP(hipMemcpy(s->d_perm, perm.data(), sizeof(int) * perm.size(), hipMemcpyHostToDevice));
     }
     if (s->rng == mh::RNG_CURAND_XORWOW) {
-        MH_TRY_HIP(hipMalloc((void**)&s->d_xw, sizeof(unsigned int) * 6 * nc));
+        if (!ensure(&s->d_xw, s->cap_xw, (size_t)6 * nc)) return false;
         MH_TRY_HIP(mh::launch_xorwow_init(s->seed, s->chain_offset, s->n_chains, s->d_xw, s->stream));
     }
-    MH_TRY_HIP(hipMalloc((void**)&s->d_meta, sizeof(mh::ChainMeta) * nc));
-    MH_TRY_HIP(hipMalloc((void**)&s->d_pts, sizeof(point) * n * nc));
-    MH_TRY_HIP(hipMalloc((void**)&s->d_costs, sizeof(resultCosts) * nc));
-    MH_TRY_HIP(hipMalloc((void**)&s->d_summary, sizeof(mh_summary)));
+    if (!ensure(&s->d_meta, s->cap_meta, (size_t)nc)) return false;
+    if (!ensure(&s->d_pts, s->cap_pts, n * nc)) return false;
+    if (!ensure(&s->d_costs, s->cap_costs, (size_t)nc)) return false;
+    if (!ensure(&s->d_summary, s->cap_summary, 1)) return false;
     MH_TRY_HIP(mh::launch(mh::OP_INIT, s->args(), s->geo.L, s->geo.npl, s->geo.waves, s->stream));
     return record_done(s, s->stream);
 }
@@ -601,15 +638,101 @@ bool lock_host(void* p, size_t bytes) {
     return false;
 }
 
+// ---- KernelWrapper's session cache -----------------------------------------------------------
+// A KernelWrapper call runs one session per device: a stream and an event, a dozen device
+// buffers, the geometry (occupancy queries), the room upload, then the launches and the copy
+// back. Creating and destroying all of that on every call cost a fixed ~7 ms (round 4: config
+// 2's shape took 12.6 ms per call for 5.3 ms of kernels). A call now borrows a session from a
+// per-device pool and gives it back after its download: stream, event and buffers are reused
+// (a buffer grows only when a call needs more) and the geometry is kept while the room's shape
+// and the chain count stay the same. Thread-safe: a mutex per device, and concurrent calls
+// borrow different sessions (at most kPoolKeep idle ones are kept per device). The pool is never
+// destroyed: freeing device memory from a static destructor would run after the HIP runtime's
+// own teardown; the process's exit releases it. $MH_WRAPPER_CACHE=0 turns the cache off.
+constexpr int kPoolDevices = 64;
+constexpr size_t kPoolKeep = 2;
+
+struct SessionPool {
+    std::mutex mu;
+    std::vector<mh_session*> idle;
+};
+
+SessionPool* session_pools() {
+    static SessionPool* pools = new SessionPool[kPoolDevices];
+    return pools;
+}
+
+bool wrapper_cache_on() {
+    static const bool on = !(getenv("MH_WRAPPER_CACHE") && atoi(getenv("MH_WRAPPER_CACHE")) == 0);
+    return on;
+}
+
+bool configure_session(mh_session* s, const Room& room, int device, int64_t n_chains,
+                       int64_t chain_offset, const mh_options& o);
+
+// A set-up session for a KernelWrapper shard: an idle pooled one if the device has one.
+mh_session* session_borrow(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
+                           const mh_options& o) {
+    mh_session* s = nullptr;
+    if (wrapper_cache_on() && device >= 0 && device < kPoolDevices) {
+        SessionPool& p = session_pools()[device];
+        std::lock_guard<std::mutex> lk(p.mu);
+        if (!p.idle.empty()) {
+            s = p.idle.back();
+            p.idle.pop_back();
+        }
+    }
+    if (!s) s = new mh_session();
+    if (!configure_session(s, room, device, n_chains, chain_offset, o)) {
+        std::string e = g_last_error;
+        free_session(s);
+        set_error(e);
+        return nullptr;
+    }
+    return s;
+}
+
+// Back to the pool after a complete call (its work is downloaded and synchronised).
+void session_give_back(mh_session* s) {
+    if (!s) return;
+    if (wrapper_cache_on() && s->device >= 0 && s->device < kPoolDevices) {
+        SessionPool& p = session_pools()[s->device];
+        std::lock_guard<std::mutex> lk(p.mu);
+        if (p.idle.size() < kPoolKeep) {
+            p.idle.push_back(s);
+            return;
+        }
+    }
+    free_session(s);
+}
+
 mh_session* session_create(const Room& room, int device, int64_t n_chains, int64_t chain_offset,
                            const mh_options& o) {
+    mh_session* s = new mh_session();
+    if (!configure_session(s, room, device, n_chains, chain_offset, o)) {
+        std::string e = g_last_error;
+        free_session(s);
+        set_error(e);
+        return nullptr;
+    }
+    return s;
+}
+
+// Options, room and chains into a session (new or pooled), then its set-up.
+bool configure_session(mh_session* s, const Room& room, int device, int64_t n_chains,
+                       int64_t chain_offset, const mh_options& o) {
     const int K = o.n_temps > 1 ? o.n_temps : 1;
     if (K > 1 && (n_chains % K != 0 || chain_offset % K != 0)) {
         set_error("parallel tempering: the chain count and offset must be multiples of n_temps");
-        return nullptr;
+        return false;
     }
     const uint64_t seed = o.seed;
-    mh_session* s = new mh_session();
+    if (s->device != device) {  // (a pooled session stays on its device; a new one starts at 0)
+        if (s->stream || s->done) {
+            set_error("internal: a session cannot change device");
+            return false;
+        }
+    }
     s->track = o.track_best;
     s->rng = o.rng;
     s->n_temps = K;
@@ -623,13 +746,7 @@ mh_session* session_create(const Room& room, int device, int64_t n_chains, int64
     s->n_chains = n_chains;
     s->chain_offset = chain_offset;
     s->seed = seed;
-    if (!session_init(s)) {
-        std::string e = g_last_error;
-        free_session(s);
-        set_error(e);
-        return nullptr;
-    }
-    return s;
+    return session_init(s);
 }
 
 // The devices a KernelWrapper call shards over: $MH_DEVICES ("all", or a comma list of device
@@ -740,15 +857,19 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
     const bool locked_pts = lock_host(pts, sizeof(point) * n * (size_t)chains);
     const bool locked_costs = lock_host(costs.data(), sizeof(resultCosts) * (size_t)chains);
     auto work = [&](Shard& sh) {
-        mh_session* s = session_create(room, sh.device, sh.count, sh.begin, opts);
+        mh_session* s = session_borrow(room, sh.device, sh.count, sh.begin, opts);
         if (!s) {
             sh.err = g_last_error;
             return;
         }
         sh.ok = session_run(s, iterations, s->stream) && session_finalize(s, s->stream) &&
                 session_download(s, pts + n * sh.begin, costs.data() + sh.begin, true);
-        if (!sh.ok) sh.err = g_last_error;
-        free_session(s);
+        if (!sh.ok) {
+            sh.err = g_last_error;
+            free_session(s);  // (a failed session is not reused)
+        } else {
+            session_give_back(s);
+        }
     };
     if (shards.size() == 1) {
         work(shards[0]);

@@ -181,6 +181,108 @@ __device__ __forceinline__ void append4(const Staged<double>& S, int& pos, float
     pos += tot;
 }
 
+// ---- speculation trees ----------------------------------------------------------------------
+// A batch evaluates the K nodes of a prefix-closed tree of accept / reject histories. Node g
+// (group g) evaluates the proposal of step t + dep(g) against the configuration its history
+// leaves -- the batch's incoming state with the proposals of the steps it accepted applied in
+// order -- and its Accept compares with the total of the node whose proposal that configuration
+// is (cpar), or the incoming total. The realised path walks from the root by Accept's decisions
+// until it leaves the tree; its steps commit. Every decision on the path is Accept's on exact
+// costs of the configuration the sequential chain holds there, so any prefix-closed tree gives
+// the sequential chain bit for bit; the shape only sets how many steps a batch commits: with
+// acceptance rate p, the sum of its nodes' path probabilities, largest for the K most probable
+// histories. (Round 4's linear speculation is the all-reject path; at config 2's p = 0.41 it
+// commits 2.46 steps per batch, the tree {root, R, A, RR, RA, AR, RRR, AA} 3.22.)
+struct SpecTree {
+    uint32_t dep;       // 4 bits per node: its step's offset in the batch
+    uint64_t hist;      // 8 bits per node: bit i set = step t + i accepted on its history
+    uint32_t cpar;      // 4 bits per node: the node whose configuration is its current one
+                        // (15: the batch's incoming state)
+    uint32_t cha, chr;  // 4 bits per node: the next node on an accept / a reject (15: none)
+    int maxdep;
+};
+
+// The K most probable histories for acceptance rate p, grown best-first from the root (a child
+// is less probable than its parent, so the set is prefix-closed). Wave-uniform.
+__device__ __forceinline__ SpecTree spec_tree(float p) {
+    p = fminf(fmaxf(p, 0.02f), 0.98f);
+    float pr[K];
+    int dp[K], cp[K], ca[K], cr[K];
+    uint32_t hs[K];
+    pr[0] = 1.0f;
+    dp[0] = 0;
+    hs[0] = 0u;
+    cp[0] = ca[0] = cr[0] = 15;
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+        float best = -1.0f;
+        int bi = 0, bb = 0;
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const bool open = (b ? ca[i] : cr[i]) == 15;
+                const float q = pr[i] * (b ? p : 1.0f - p);
+                const bool take = open && q > best;
+                best = take ? q : best;
+                bi = take ? i : bi;
+                bb = take ? b : bb;
+            }
+        }
+        int pdp = 0, pcp = 15;
+        uint32_t phs = 0u;
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+            if (i == bi) {
+                pdp = dp[i];
+                phs = hs[i];
+                pcp = cp[i];
+                if (bb) ca[i] = k;
+                else cr[i] = k;
+            }
+        }
+        pr[k] = best;
+        dp[k] = pdp + 1;
+        hs[k] = phs | ((uint32_t)bb << pdp);
+        cp[k] = bb ? bi : pcp;
+        ca[k] = cr[k] = 15;
+    }
+    SpecTree t;
+    t.dep = t.cpar = t.cha = t.chr = 0u;
+    t.hist = 0ull;
+    t.maxdep = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        t.dep |= (uint32_t)dp[k] << (4 * k);
+        t.hist |= (uint64_t)hs[k] << (8 * k);
+        t.cpar |= (uint32_t)cp[k] << (4 * k);
+        t.cha |= (uint32_t)ca[k] << (4 * k);
+        t.chr |= (uint32_t)cr[k] << (4 * k);
+        t.maxdep = max(t.maxdep, dp[k]);
+    }
+    t.dep = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.dep);
+    t.hist = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(t.hist >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t.hist);
+    t.cpar = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.cpar);
+    t.cha = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.cha);
+    t.chr = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.chr);
+    t.maxdep = __builtin_amdgcn_readfirstlane(t.maxdep);
+    return t;
+}
+
+// Position of the q-th set bit (q from 0) of a 16-bit mask: a branch-free binary search.
+__device__ __forceinline__ int nth_bit(uint32_t m, int q) {
+    int pos = 0;
+    int c = __builtin_popcount(m & 0xffu);
+    if (q >= c) { q -= c; m >>= 8; pos += 8; }
+    c = __builtin_popcount(m & 0xfu);
+    if (q >= c) { q -= c; m >>= 4; pos += 4; }
+    c = __builtin_popcount(m & 0x3u);
+    if (q >= c) { q -= c; m >>= 2; pos += 2; }
+    if (q >= (int)(m & 1u)) pos += 1;
+    return pos;
+}
+
 __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = __lane_id();
@@ -300,7 +402,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     // (LDS shared between lanes moves through Staged / Published views, mh_common.h)
     const Staged<ObjP> Pst{X->P[g]};
     const Staged<double> RYst{X->RY[g]};
-    const Staged<double> Sst{X->S[g]};
+    const Staged<double> Sall{&X->S[0][0]};  // every group's streams (group g at g * S_END)
     const Staged<double> XDst{X->XD[g]}, YDst{X->YD[g]};
     const Staged<int> STOP{&SH->stop};
     if (r < n) {
@@ -382,6 +484,18 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 
     unsigned int accepted = 0;
     const float rx_sx = rm.sx, rx_sy = rm.sy;
+    // The batch's tree (spec_tree), rebuilt every 32 batches from this launch's acceptance rate
+    // (a prior of 2 accepts in 5 steps to start). Each lane's node is its group's.
+    SpecTree tr;
+    int my_dep = 0, my_hist = 0, my_cpar = 15;
+    auto set_tree = [&](float p) __attribute__((always_inline)) {
+        tr = spec_tree(p);
+        my_dep = (int)((tr.dep >> (4 * g)) & 15u);
+        my_hist = (int)((tr.hist >> (8 * g)) & 255u);
+        my_cpar = (int)((tr.cpar >> (4 * g)) & 15u);
+    };
+    set_tree(0.4f);
+    unsigned int batches = 0;
 #if MH_STAMPS
     unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
@@ -393,7 +507,10 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             publish_workgroup(STOP);
             break;
         }
-        int kb = min(K, a.iterations - done);
+        if ((++batches & 31u) == 0u)
+            set_tree((float)(accepted + 2u) / (float)(done + 5));
+        // steps this batch can reach: the tree's depth, the launch's remaining steps
+        int kb = min(tr.maxdep + 1, a.iterations - done);
         // At most ~5 draws per step (more only for frozen-object redraws, which then draw past
         // the window directly): refill unless 48 remain.
         if (off > 128 - 48) {
@@ -407,8 +524,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         // takes one pair either way (h unchanged, the pair's second normal cached when h = 1),
         // rotate one pair when h = 0 (then cached) and none when h = 1, swap none. So lane i
         // parses the mode and picks of a step starting at off + i, and a wave-uniform walk of
-        // at most 8 hops chains the batch's steps; a step starting past off + 63 (or past word
-        // 123) ends the batch early.
+        // at most kb hops chains the batch's steps; a step starting past off + 63 (or past word
+        // 123) ends the batch early. None of this depends on a decision.
         int pmode = 3, pk1 = -1, pk2 = -1, pafter = 0;  // (3: not parsed, the walk stops there)
         {
             const unsigned int o0 = off + (unsigned int)lane;
@@ -432,41 +549,42 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         SSTAMP(8);
         // The walk: state (o, h, cache position: -1 = the batch's incoming cached normal), all
         // wave-uniform (readfirstlane keeps it in scalar registers), branch-free: one readlane of
-        // the packed parse per hop.
+        // the packed parse per hop. Group s keeps step s's start, next start, h and cache.
         const int pk = pmode | (pafter << 2);
-        unsigned int go = off, gnext = off + 1;  // lanes of group s: step s's start and the next's
-        int gh = 0, gcp = -1;                    // and step s's cache flag and position
+        unsigned int go = off, gnext = off + 1;
+        int gh = 0, gcp = -1;
         const unsigned int off_s = (unsigned int)__builtin_amdgcn_readfirstlane((int)off);
         unsigned int wo = off_s;
         int wh = __builtin_amdgcn_readfirstlane(bmh), wcp = -1;
         int kw = __builtin_amdgcn_readfirstlane(kb);
 #pragma unroll
         for (int s = 0; s < K; ++s) {
+            if (s >= kw) break;
             const int i = __builtin_amdgcn_readfirstlane((int)(wo - off_s));
             const int v = __builtin_amdgcn_readlane(pk, i & 63);
-            const int md = (i < 64 && s < kw) ? (v & 3) : 3;
-            kw = (md == 3 && s < kw) ? s : kw;
+            const int md = i < 64 ? (v & 3) : 3;
+            kw = md == 3 ? s : kw;
             go = g == s ? wo : go;
             gh = g == s ? wh : gh;
             gcp = g == s ? wcp : gcp;
             const int pa = v >> 2;
-            const bool tr = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
-            const bool pair = tr || (ro && !wh);    // the step takes a Box-Muller pair
-            wcp = (tr && wh) || (ro && !wh) ? pa : wcp;  // ... and caches its second
+            const bool tr_ = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
+            const bool pair = tr_ || (ro && !wh);    // the step takes a Box-Muller pair
+            wcp = (tr_ && wh) || (ro && !wh) ? pa : wcp;  // ... and caches its second
             wo = md == 3 ? wo : (unsigned int)pa + (pair ? 3u : 1u);
             wh = ro ? !wh : wh;
             gnext = g == s ? wo : gnext;
         }
         kb = kw;
-        if (g >= kb) {  // (groups past the batch: harmless reads)
+        if (g >= kb) {  // (groups past the batch's steps: harmless reads)
             go = off;
             gnext = off + 1;
             gcp = -1;
         }
         SSTAMP(9);
-        // Group g's step from lane (start - off)'s parse, its normals and Accept's uniform.
+        // Group s's record of step s from lane (start - off)'s parse, its normals and Accept's
+        // uniform; every group then reads the records it applies by readlane (wave-uniform).
         SpecRec R;
-        R.live = g < kb;
         float bv_out;  // the cached second normal after the step (when h_out)
         int h_out;
         {
@@ -505,41 +623,50 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 R.k2 = -1;
             }
             R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
+            R.live = g < kb;
             R.pad = 0.0f;
         }
         SSTAMP(1);
-        const bool live = R.live != 0;
-        const int k1 = live ? R.k1 : -1, k2 = live ? R.k2 : -1;
-
-        // Apply group g's proposal to its copy (Kernel.cu:576-704).
+        // Group g's configuration: the incoming state with the proposals of the steps its
+        // history accepted and then its own step's applied in step order (Kernel.cu:576-704;
+        // each is the reference's edit of cfgStar, made on the configuration it would see).
         double sx = cx, sy = cy, sry = cry;
-        bool moved = false;
-        if (live && R.mode == 0 && r == k1) {
-            moved = true;
-            if (sx + (double)R.d1 > rm.rmax_x) sx = rm.rmax_x;
-            else if (sx + (double)R.d1 < rm.rmin_x) sx = rm.rmin_x;
-            else sx = sx + (double)R.d1;
-            if (sy + (double)R.d2 > rm.rmax_y) sy = rm.rmax_y;
-            else if (sy + (double)R.d2 < rm.rmin_y) sy = rm.rmin_y;
-            else sy = sy + (double)R.d2;
-        } else if (live && R.mode == 1 && r == k1) {
-            moved = true;
-            sry = sry + (double)R.d1;
-            if (sry < 0) sry = sry + kTwoPI;
-            else if (sry > kTwoPI) sry = sry - kTwoPI;
-        }
-        if (__ballot(live && R.mode == 2 && k1 >= 0)) {  // (every lane active for the shuffles)
-            const int ia = gbase + (k1 >= 0 ? k1 : 0), ib = gbase + (k2 >= 0 ? k2 : 0);
-            const double ax = shfl_d(cx, ia), ay = shfl_d(cy, ia), ary = shfl_d(cry, ia);
-            const double bx = shfl_d(cx, ib), by = shfl_d(cy, ib), bry = shfl_d(cry, ib);
-            if (live && R.mode == 2 && k1 >= 0) {
+        bool moved = false;  // this lane's object differs from the incoming state
+        for (int i = 0; i < kb; ++i) {  // (wave-uniform: the step's record by readlane)
+            const bool app = i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
+            const int md = __builtin_amdgcn_readlane(R.mode, i << 3);
+            const int q1 = __builtin_amdgcn_readlane(R.k1, i << 3);
+            const int q2 = __builtin_amdgcn_readlane(R.k2, i << 3);
+            const float e1 = readlane_f(R.d1, i << 3);
+            if (md == 0) {  // translate
+                const float e2 = readlane_f(R.d2, i << 3);
+                if (app && r == q1) {
+                    moved = true;
+                    if (sx + (double)e1 > rm.rmax_x) sx = rm.rmax_x;
+                    else if (sx + (double)e1 < rm.rmin_x) sx = rm.rmin_x;
+                    else sx = sx + (double)e1;
+                    if (sy + (double)e2 > rm.rmax_y) sy = rm.rmax_y;
+                    else if (sy + (double)e2 < rm.rmin_y) sy = rm.rmin_y;
+                    else sy = sy + (double)e2;
+                }
+            } else if (md == 1) {  // rotate
+                if (app && r == q1) {
+                    moved = true;
+                    sry = sry + (double)e1;
+                    if (sry < 0) sry = sry + kTwoPI;
+                    else if (sry > kTwoPI) sry = sry - kTwoPI;
+                }
+            } else if (q1 >= 0) {  // swap (every lane active for the shuffles)
+                const int ia = gbase + q1, ib = gbase + q2;
+                const double ax = shfl_d(sx, ia), ay = shfl_d(sy, ia), ary = shfl_d(sry, ia);
+                const double bx = shfl_d(sx, ib), by = shfl_d(sy, ib), bry = shfl_d(sry, ib);
                 // object 1 takes object 2's pose, object 2 object 1's through float temporaries
-                if (r == k2) {
+                if (app && r == q2) {
                     sx = (double)(float)ax;
                     sy = (double)(float)ay;
                     sry = (double)(float)ary;
                     moved = true;
-                } else if (r == k1) {
+                } else if (app && r == q1) {
                     sx = bx;
                     sy = by;
                     sry = bry;
@@ -564,58 +691,63 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         SSTAMP(2);
         const ObjP* Pg = pv.a.ptr();
 
-        // Per-object terms of the proposal's configuration.
-        float cphs = cph;
-        double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
-        const bool t0 = r < nr && touches(H->rel[r], k1, k2);
-        const bool t1 = r + GL < nr && touches(H->rel[r + GL], k1, k2);
-        {  // the exact FocalPoint and relationship terms
-            if (nr + 2 <= GL) {
-                // One atan2 per lane: lane r < nr for relationship r, lanes nr and nr + 1 for the
-                // FocalPoint terms of the moved objects k1 and k2; the cosines go back to them.
-                const int fo = r == nr ? k1 : (r == nr + 1 ? k2 : -1);
-                const bool foc = fo >= 0;
-                const ObjP q = Pg[foc ? fo : 0];
-                double ay = 0.0, ax = 1.0;
-                float ti = 0.0f;
-                if (t0) pw0 = rel_pair(H->rel[r], Pg, ay, ax, ti);
-                if (foc) {
-                    ay = (double)(rm.fyf - q.yf);
-                    ax = (double)(rm.fxf - q.xf);
-                }
-                float cf = 0.0f;
-                if (__ballot(foc || t0)) {
-                    const double at = atan2_ool(ay, ax);
-                    if (t0) an0 = rel_angle(H->rel[r], at, ti);
-                    if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
-                        const float b = (float)at - q.rotYf;
-                        cf = cos_f32((float)((double)b + kHalfPI));
-                    }
-                }
-                const float c1 = shfl_f(cf, gbase + nr), c2 = shfl_f(cf, gbase + nr + 1);
-                if (moved) cphs = r == k2 ? c2 : c1;  // (a swap's k2 branch wins, as in the apply)
-            } else if (__ballot(moved || t0 || t1)) {
-                if (moved) cphs = focal_cos(rm, xf, yf, ryf);
-                if (t0) rel_exact(H->rel[r], Pg, pw0, an0);
-                if (t1) rel_exact(H->rel[r + GL], Pg, pw1, an1);
-            }
-        }
-        SSTAMP(3);
-        if (r < n) {
-            const float area = __int_as_float(H->objs[r].pad);
-            Sst.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
-            Sst.put(S_VBY + r, (double)area * sy);
-            Sst.put(S_FP + r, -(double)cphs);
-        }
+        // The exact FocalPoint terms of the group's moved objects and the terms of the
+        // relationships they touch, the rest carried from the incoming state. The group's
+        // jobs (touched relationships first, then moved objects) are dealt out to its 8 lanes,
+        // one double atan2 per lane per pass (Kernel.cu:170-188, 222, 249-253, 271-277).
+        const uint32_t mv = (uint32_t)group_ballot<GL>(moved && r < n, gbase);
+        bool t0 = false, t1 = false;
         if (r < nr) {
-            Sst.put(S_PW + r, -pw0);
-            Sst.put(S_ANG + r, -an0);
+            const RelConst& rc = H->rel[r];
+            t0 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
         if (r + GL < nr) {
-            Sst.put(S_PW + r + GL, -pw1);
-            Sst.put(S_ANG + r + GL, -an1);
+            const RelConst& rc = H->rel[r + GL];
+            t1 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
-        const Published<double> Sv = publish(Sst);
+        const uint32_t tm = (uint32_t)group_ballot<GL>(t0, gbase) |
+                            ((uint32_t)group_ballot<GL>(t1, gbase) << GL);
+        const int nrt = __builtin_popcount(tm), jobs = nrt + __builtin_popcount(mv);
+        const Staged<double> Sg = Sall.at(g * S_END);
+        if (r < n) {
+            const float area = __int_as_float(H->objs[r].pad);
+            Sg.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
+            Sg.put(S_VBY + r, (double)area * sy);
+            if (!moved) Sg.put(S_FP + r, -(double)cph);
+        }
+        if (r < nr && !t0) {
+            Sg.put(S_PW + r, -rpw0);
+            Sg.put(S_ANG + r, -rang0);
+        }
+        if (r + GL < nr && !t1) {
+            Sg.put(S_PW + r + GL, -rpw1);
+            Sg.put(S_ANG + r + GL, -rang1);
+        }
+        for (int q = r; __ballot(q < jobs) != 0; q += GL) {  // (wave-uniform trip count)
+            const bool has = q < jobs, isrel = q < nrt;
+            const int idx = nth_bit(isrel ? tm : mv, isrel ? q : q - nrt);
+            const bool rel = has && isrel, foc = has && !isrel;
+            const RelConst& rc = H->rel[rel ? idx : 0];
+            const ObjP qo = Pg[foc ? idx : 0];
+            double ay = 0.0, ax = 1.0, pw = 0.0;
+            float ti = 0.0f;
+            if (rel) pw = rel_pair(rc, Pg, ay, ax, ti);
+            if (foc) {
+                ay = (double)(rm.fyf - qo.yf);
+                ax = (double)(rm.fxf - qo.xf);
+            }
+            const double at = atan2_ool(ay, ax);
+            if (rel) {
+                Sg.put(S_PW + idx, -pw);
+                Sg.put(S_ANG + idx, -rel_angle(rc, at, ti));
+            }
+            if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
+                const float b = (float)at - qo.rotYf;
+                Sg.put(S_FP + idx, -(double)cos_f32((float)((double)b + kHalfPI)));
+            }
+        }
+        const Published<double> Sv = publish(Sall);
+        SSTAMP(3);
         SSTAMP(4);
         SSTAMP(5);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
@@ -633,7 +765,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 case 6: base = S_PW; len = nr; rnd = false; break;
                 default: base = S_ANG; len = nr; rnd = false; break;
             }
-            const double* src = Sv.ptr() + base;
+            const double* src = Sv.ptr() + g * S_END + base;
             double acc = 0.0;
             for (int l = 0; l < len; ++l) {
                 const double s = acc + src[l];
@@ -667,42 +799,68 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             t = t + sc[7];
             sc[0] = t;
         }
-        // Accept (Kernel.cu:706-713) for every live proposal against the current total; the
-        // first accepted one ends the batch.
-        const bool acc_g = live && R.u < accept_threshold(kBeta * ((double)sc[0] - (double)cur[0]));
-        const uint64_t bal = __ballot(acc_g && r == 0);
-        const int gs = bal ? (int)(__builtin_ctzll(bal) >> 3) : -1;
-        const int committed = gs >= 0 ? gs + 1 : kb;
-        if (gs >= 0) {
-            const int src = (gs << 3) + r;
+        // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
+        // total (the node whose configuration it started from, or the batch's incoming total).
+        const float u_g = shfl_f(R.u, my_dep << 3);
+        const float cp_tot = shfl_f(sc[0], (my_cpar == 15 ? 0 : my_cpar) << 3);
+        const float cur_g = my_cpar == 15 ? cur[0] : cp_tot;
+        const bool acc_g = my_dep < kb && u_g < accept_threshold(kBeta * ((double)sc[0] - (double)cur_g));
+        const uint64_t ab = __ballot(acc_g && r == 0);
+        // The realised path from the root: its nodes' steps commit; the configuration after
+        // them is the last accepted node's (or the incoming one).
+        int node = 0, steps = 0, last = 15, nacc = 0;
+        unsigned int acc_steps = 0;
+#pragma unroll
+        for (int d = 0; d < K; ++d) {
+            if (node == 15 || d >= kb) break;
+            ++steps;
+            const bool an = ((ab >> (node << 3)) & 1ull) != 0;
+            if (an) {
+                last = node;
+                ++nacc;
+                acc_steps |= 1u << d;
+            }
+            node = (int)(((an ? tr.cha : tr.chr) >> (4 * node)) & 15u);
+        }
+        if (last != 15) {
+            const int src = (last << 3) + r;
             cx = shfl_d(sx, src);
             cy = shfl_d(sy, src);
             cry = shfl_d(sry, src);
-            cph = shfl_f(cphs, src);
-            rpw0 = shfl_d(pw0, src);
-            rang0 = shfl_d(an0, src);
-            rpw1 = shfl_d(pw1, src);
-            rang1 = shfl_d(an1, src);
+            const double* sl = Sv.ptr() + last * S_END;
+            if (r < n) cph = (float)(-sl[S_FP + r]);
+            if (r < nr) {
+                rpw0 = -sl[S_PW + r];
+                rang0 = -sl[S_ANG + r];
+            }
+            if (r + GL < nr) {
+                rpw1 = -sl[S_PW + r + GL];
+                rang1 = -sl[S_ANG + r + GL];
+            }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], gs << 3);
-            ++accepted;
+            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last << 3);
+            accepted += (unsigned int)nacc;
             // An accepted swap also exchanges z, rotX and rotZ (:675-700), object 1's values
-            // through float temporaries; no cost reads them, so they live in HBM only.
-            const int smode = __builtin_amdgcn_readlane(R.mode, gs << 3);
-            const int sk1 = __builtin_amdgcn_readlane(R.k1, gs << 3);
-            const int sk2 = __builtin_amdgcn_readlane(R.k2, gs << 3);
-            if (smode == 2 && sk1 >= 0 && lane == 0) {
+            // through float temporaries; no cost reads them, so they live in HBM only (in step
+            // order: a later swap sees an earlier one's values).
+            for (int d = 0; d < steps; ++d) {
+                if (!((acc_steps >> d) & 1u)) continue;
+                const int smode = __builtin_amdgcn_readlane(R.mode, d << 3);
+                const int sk1 = __builtin_amdgcn_readlane(R.k1, d << 3);
+                const int sk2 = __builtin_amdgcn_readlane(R.k2, d << 3);
+                if (smode == 2 && sk1 >= 0 && lane == 0) {
 #pragma unroll
-                for (int f = 0; f < 3; ++f) {
-                    double* row = st + (F_Z + f) * n;
-                    const double va = row[sk1], vb = row[sk2];
-                    row[sk1] = vb;
-                    row[sk2] = (double)(float)va;
+                    for (int f = 0; f < 3; ++f) {
+                        double* row = st + (F_Z + f) * n;
+                        const double va = row[sk1], vb = row[sk2];
+                        row[sk1] = vb;
+                        row[sk2] = (double)(float)va;
+                    }
                 }
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0) {  // [done, kb, off, bmh, gs, committed, cur0], per group 8 words
+        if (chain == 0) {  // [done, kb, off, bmh, last, steps, cur0], per group 8 words
             const unsigned int base = g_spec_dbg_n;
             if (base + 7 + 8 * K < (1u << 16)) {
                 if (lane == 0) {
@@ -710,8 +868,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                     g_spec_dbg[base + 1] = (unsigned)kb;
                     g_spec_dbg[base + 2] = off;
                     g_spec_dbg[base + 3] = (unsigned)bmh;
-                    g_spec_dbg[base + 4] = (unsigned)gs;
-                    g_spec_dbg[base + 5] = (unsigned)committed;
+                    g_spec_dbg[base + 4] = (unsigned)last;
+                    g_spec_dbg[base + 5] = (unsigned)steps;
                     g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
                 }
                 if (r == 0) {
@@ -730,14 +888,14 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
 #endif
         // The stream's state after the committed steps: what the last of them leaves.
-        off = (unsigned int)__builtin_amdgcn_readlane((int)gnext, (committed - 1) << 3);
-        bmh = __builtin_amdgcn_readlane(h_out, (committed - 1) << 3);
-        bmv = readlane_f(bv_out, (committed - 1) << 3);
-        done += committed;
+        off = (unsigned int)__builtin_amdgcn_readlane((int)gnext, (steps - 1) << 3);
+        bmh = __builtin_amdgcn_readlane(h_out, (steps - 1) << 3);
+        bmv = readlane_f(bv_out, (steps - 1) << 3);
+        done += steps;
         SSTAMP(7);
 #if MH_STAMPS
         cyc[14] += 1;
-        cyc[15] += (unsigned long long)committed;
+        cyc[15] += (unsigned long long)steps;
 #endif
     }
 #if MH_STAMPS

@@ -315,16 +315,19 @@ def test_index_n_pick_redrawn(mh, orc, hiplib, monkeypatch, case, path):
     check_chains(f"index-n chain {cid} ({path[0]})", pts, costs, rp, rc, ids=[cid])
 
 
-@pytest.mark.parametrize("path", STEP_PATHS, ids=[p[0] for p in STEP_PATHS])
-@pytest.mark.parametrize("case", GOLDEN["u1_accept"], ids=lambda c: f"N{c['n']}-chain{c['chain']}")
+# (the speculative kernel serves rooms of at most 8 objects: only the N = 8 fixture reaches it)
+U1_CASES = [(c, p) for c in GOLDEN["u1_accept"] for p in STEP_PATHS
+            if p[0] != "speculative" or c["n"] <= 8]
+
+
+@pytest.mark.parametrize("case,path", U1_CASES,
+                         ids=[f"N{c['n']}-chain{c['chain']}-{p[0]}" for c, p in U1_CASES])
 def test_accept_draw_one_rejects_uphill(mh, orc, hiplib, monkeypatch, case, path):
     """A chain whose Accept draws u == 1.0f (the (0, 1] uniform's top value) against an uphill
     proposal: the threshold min(1, exp(...)) is exactly 1, so Accept rejects (Kernel.cu:706-713).
     The rejection bound must not certainly accept it (round 2's bound did; found by
     tools/bound_check.py). Fixture from tests/golden/find_u1_accept.py; bit for bit against the
     oracle on every step kernel and RNG path."""
-    if path[0] == "speculative" and case["n"] > 8:
-        pytest.skip("the speculative kernel serves rooms of at most 8 objects")
     for k, v in path[1].items():
         monkeypatch.setenv(k, v)
     room = mh.synthetic_room(case["n"])
@@ -401,3 +404,33 @@ def _nonzero_clearance_pairs(room, pts):
         for b in objs:
             cnt += max(a[0], b[0]) < min(a[2], b[2]) and max(a[1], b[1]) < min(a[3], b[3])
     return cnt
+
+
+def test_kernelwrapper_pooled_sessions(mh, orc, hiplib):
+    """KernelWrapper reuses its per-device sessions across calls (mh_abi.cpp "session cache"):
+    the stream, buffers and geometry of one call serve the next. A sequence that grows and
+    shrinks the room, the chain count and the options -- each call checked bit for bit against
+    the oracle -- shows no state leaks from one call into the next."""
+    calls = [  # (objects, chains, steps, seed, kwargs)
+        (8, 256, 300, 11, {}),
+        (64, 96, 120, 12, {}),                       # larger room, fewer chains
+        (8, 1024, 200, 13, {}),                      # more chains than any buffer so far
+        (8, 256, 300, 11, {}),                       # the first call again: same result
+        (16, 128, 150, 14, {"track": mh.abi.MH_TRACK_LOWEST}),
+        (16, 128, 150, 15, {"rng": mh.abi.MH_RNG_CURAND_XORWOW}),
+        (12, 120, 160, 16, {"temps": 4, "swap_interval": 10, "beta_min": 0.5}),
+        (5, 64, 0, 17, {}),                          # zero steps: the input poses
+    ]
+    first = None
+    for n, chains, steps, seed, kw in calls:
+        room = mh.synthetic_room(n)
+        pts, costs = mh.kernel_wrapper(room, chains, steps, seed=seed, **kw)
+        okw = {k: v for k, v in kw.items()}
+        if "rng" in okw:
+            okw["rng"] = 1
+        rp, rc, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS, **okw)
+        check_chains(f"pooled KernelWrapper N={n} {chains}x{steps} {kw}", pts, costs, rp, rc)
+        if first is None:
+            first = (pts, costs)
+        elif (n, chains, steps, seed, kw) == calls[0]:
+            assert np.array_equal(pts.view(np.uint32), first[0].view(np.uint32))
