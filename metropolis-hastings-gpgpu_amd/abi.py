@@ -330,7 +330,7 @@ def debug_rng(seed: int, subsequence: int, n: int, rng: int = MH_RNG_PHILOX):
 
 
 # doubles each probe writes per argument (mh_math.h mh_probe_width: the sincos probes 2)
-MH_PROBE_COUNT = 11
+MH_PROBE_COUNT = 12
 _PROBE_WIDTH = {1: 2, 4: 2}  # MH_PROBE_BM_SINCOS, MH_PROBE_XW_SINCOS
 
 

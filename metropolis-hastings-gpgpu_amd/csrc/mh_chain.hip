@@ -1946,7 +1946,14 @@ __global__ void __launch_bounds__(256) mh_math_kernel(int fn, uint64_t start, ui
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += stride) {
         double r[2];
-        mh_math_probe(fn, start + k, r);
+        if (fn == MH_PROBE_ACCEPT) {  // the device's decision is the screened one (accept_u)
+            float u;
+            double x;
+            mh_arg_accept(start + k, &u, &x);
+            r[0] = accept_u(u, x) ? 1.0 : 0.0;
+        } else {
+            mh_math_probe(fn, start + k, r);
+        }
         out[k * w] = r[0];
         if (w == 2) out[k * w + 1] = r[1];
     }

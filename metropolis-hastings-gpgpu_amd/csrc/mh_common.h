@@ -1268,6 +1268,22 @@ __device__ __forceinline__ float accept_threshold(double x) {
     return fminf(1.0f, (float)exp_ool(x));
 }
 
+// Accept's decision u < accept_threshold(x), screened in fp32. For -24 <= x < 0, e = v_exp_f32(
+// (float)x log2(e)) is within 4e-6 relative of exp(x): (float)x is off by at most 2^-20, the
+// product's rounding by 2^-24 * 35, log2(e)'s by 2^-25 relative, v_exp_f32 by 1 ulp. A u more
+// than 1e-4 relative below e is then below exp(x) (1 - 2^-24) <= (float)exp(x), and one more
+// than 1e-4 above is above (float)exp(x): decided without the double exp; only a u inside that
+// band (about 2e-4 of the draws near a threshold) evaluates it. Returns exactly
+// u < accept_threshold(x) (the accept probe, tests/test_gpu_math.py, checks 2^30 pairs).
+__device__ __forceinline__ bool accept_u(float u, double x) {
+    if (x >= 0.0) return u < 1.0f;
+    if (x < -24.0) return false;
+    const float e = __builtin_amdgcn_exp2f((float)x * 1.44269504f);
+    if (u < e * 0.9999f) return true;
+    if (u > e * 1.0001f) return false;
+    return u < fminf(1.0f, (float)exp_ool(x));
+}
+
 // Accept's decision with the proposal's exact total `star` and the current total known only as
 // the interval `cur` (after a proposal accepted on the bound): the threshold min(1, (float)exp(
 // beta (star - cur))) does not increase with cur (the double difference of two floats is

@@ -553,6 +553,31 @@ MH_MATH_FN double mh_arg_exp(uint64_t i, int kind) {
     return (double)p - (double)q;
 }
 
+/* Accept's decision u < min(1, (float)exp(x)) (Kernel.cu:712), the reference's way: x >= 0
+ * gives a threshold of exactly 1, x < -24 one below every uniform either stream draws (>= 2^-33),
+ * otherwise the double exp rounded to float. The device decides most draws with an fp32 screen
+ * instead (mh_common.h accept_u); the probe below checks the two agree. */
+MH_MATH_FN int mh_accept_exact(float u, double x) {
+    if (x >= 0.0) return u < 1.0f;
+    if (x < -24.0) return 0;
+    const float e = (float)mh_exp(x);
+    return u < (e < 1.0f ? e : 1.0f);
+}
+
+/* Arguments of the accept probe: a (0, 1] uniform as rocRAND converts a word, and x = BETA
+ * (star - cur) either within 1e-4 of log(u) (three in four: the band the screen must resolve
+ * exactly) or anywhere in [-30, 2]. */
+MH_MATH_FN void mh_arg_accept(uint64_t i, float* u, double* x) {
+    const uint64_t a = mh_mix64(i * 2 + 21), b = mh_mix64(i * 2 + 22);
+    *u = (float)(uint32_t)a * 0x1p-32f + 0x1p-33f;
+    if ((b & 3u) != 0u) {
+        const double t = ((double)(int32_t)(uint32_t)(b >> 32) * 0x1p-31) * 1e-4;
+        *x = mh_log((double)*u) + t;
+    } else {
+        *x = (double)(b >> 11) * 0x1p-53 * 32.0 - 30.0;
+    }
+}
+
 /* The numerics checks: probe `fn` at argument index i, the results as doubles (float results
  * widened exactly) in out[0] (and out[1] for the sincos probes). Exhaustive probes take i over
  * all 2^32 values; sampled ones over any range. */
@@ -568,7 +593,8 @@ enum {
     MH_PROBE_ATAN2F_BITS = 8,
     MH_PROBE_EXP_ACCEPT = 9, /* exp(BETA (star - cur)) (Accept, :712) */
     MH_PROBE_EXP_ANY = 10,
-    MH_PROBE_COUNT = 11
+    MH_PROBE_ACCEPT = 11,    /* Accept's decision, 1 or 0 (the device: its fp32 screen, :712) */
+    MH_PROBE_COUNT = 12
 };
 MH_MATH_FN int mh_probe_width(int fn) {
     return fn == MH_PROBE_BM_SINCOS || fn == MH_PROBE_XW_SINCOS ? 2 : 1;
@@ -611,6 +637,13 @@ MH_MATH_FN void mh_math_probe(int fn, uint64_t i, double* out) {
         case MH_PROBE_EXP_ANY:
             out[0] = mh_exp(mh_arg_exp(i, fn == MH_PROBE_EXP_ANY));
             break;
+        case MH_PROBE_ACCEPT: {
+            float u;
+            double xa;
+            mh_arg_accept(i, &u, &xa);
+            out[0] = mh_accept_exact(u, xa) ? 1.0 : 0.0;
+            break;
+        }
         default:
             out[0] = mh_nan();
             break;

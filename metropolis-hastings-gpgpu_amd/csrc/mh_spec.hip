@@ -52,26 +52,41 @@ constexpr int RMAX = 2 * GL;   // relationship slots (two per lane)
 constexpr int kSplit = 2;      // wavefronts per chain
 constexpr int kSpecWaves = kSplit;
 
-// Each group's ordered-sum streams (doubles, pre-signed so that every sum is acc + term):
-// VisualBalance area x and area y (Kernel.cu:200-201), FocalPoint -cos(phi) (:277), Symmetry
-// -(row max) (:314), PairWise and PairWiseAngle (:222, :249-253), the non-zero Clearance terms
-// in clearance-major order (:429) and the non-zero SurfaceArea terms (:463-479).
-enum { S_VBX = 0, S_VBY = 8, S_FP = 16, S_SYM = 24, S_PW = 32, S_ANG = 48, S_CL = 64,
-       S_SA = 128, S_END = 192 };
+// Each group's ordered-sum streams (doubles, pre-signed so that every sum is acc + term). Wave 0's:
+// VisualBalance area x and area y (Kernel.cu:200-201), FocalPoint -cos(phi) (:277), PairWise and
+// PairWiseAngle (:222, :249-253).
+enum { S_VBX = 0, S_VBY = 8, S_FP = 16, S_PW = 24, S_ANG = 24 + RMAX, S_W0 = 24 + 2 * RMAX };
+// Wave 1's: Symmetry -(row max) (:314), the non-zero Clearance terms in clearance-major order
+// (:429) and the non-zero SurfaceArea terms (:463-479).
+enum { S_SYM = 0, S_CL = 8, S_SA = 8 + GL * GL, S_W1 = 8 + GL * GL + 8 * GL };
 
-struct SpecRec {  // one step's proposal (the draws of Kernel.cu:576-704, 710)
-    int mode, k1, k2, live;
-    float d1, d2, u, pad;
+// One step of the chain's stream (the draws of Kernel.cu:576-704 and Accept's, :710): a
+// chain's draws do not depend on its decisions, so a window's steps are parsed once into these
+// records and every batch reads the ones it needs.
+constexpr int kRec = 32;  // records per window
+struct StepRec {
+    int mode, k1, k2;  // the proposal (k1 = k2 = -1: a swap of a single object draws nothing)
+    int h;             // the Box-Muller cache flag after the step
+    float d1, d2;      // translate: dx, dy; rotate: the angle
+    float u;           // Accept's uniform
+    float bv;          // the cached second normal after the step (when h)
+    unsigned int next; // window offset of the next step's first draw
+    int pad[3];
 };
 
-struct SpecChain {  // LDS of one chain
-    double S[K][S_END];    // each group's ordered-sum streams (this wavefront's)
-    float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
-    double RY[K][GL];      // each group's double rotY of every object (Symmetry, :305)
+struct SpecW0 {  // LDS of wave 0, which holds the chain
+    double S[K][S_W0];            // each group's streams
+    double RY[K][GL];             // each group's double rotY of every object (Symmetry, :305)
     double XD[K][GL], YD[K][GL];  // each group's double x, y (wave 1's symmetry and boxes)
-    ObjP P[K][GL];         // each group's float pose words
-    unsigned int wd[128];    // the 128-word window of the Philox stream
-    float bs[128], bc[128];  // Box-Muller pairs (word i, word i + 1) of the window
+    ObjP P[K][GL];                // each group's float pose words
+    unsigned int wd[128];         // the 128-word window of the Philox stream
+    float bs[128], bc[128];       // Box-Muller pairs (word i, word i + 1) of the window
+    StepRec rec[kRec];            // the window's steps
+};
+
+struct SpecW1 {  // LDS of wave 1
+    double S[K][S_W1];     // each group's streams
+    float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
 };
 
 struct SpecShared {  // LDS of the chain shared by its two wavefronts
@@ -86,8 +101,12 @@ struct SpecHdr {  // LDS of the workgroup: the room tables
 };
 
 constexpr int kSpecHdrBytes = (int)((sizeof(SpecHdr) + 15) & ~(size_t)15);
-constexpr int kSpecChainBytes = (int)((sizeof(SpecChain) + 15) & ~(size_t)15);
+constexpr int kSpecW0Bytes = (int)((sizeof(SpecW0) + 15) & ~(size_t)15);
+constexpr int kSpecW1Bytes = (int)((sizeof(SpecW1) + 15) & ~(size_t)15);
 constexpr int kSpecSharedBytes = (int)((sizeof(SpecShared) + 15) & ~(size_t)15);
+// (per chain: 9.7 + 9.7 + 1.0 KB and the 1.7 KB room tables, seven chains in a CU's 160 KB;
+// round 4's two full-size wave records took 37.5 KB, four chains per CU)
+constexpr int kSpecBytes = kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes + kSpecSharedBytes;
 
 // A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
 __device__ __attribute__((noinline)) unsigned int philox_far(uint64_t seed, uint64_t sub,
@@ -307,18 +326,18 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 
     const int64_t chain = (int64_t)blockIdx.x;  // (the whole workgroup: one chain)
     if (chain >= a.n_chains) return;
-    SpecChain* X = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes + wave * kSpecChainBytes);
-    SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSplit * kSpecChainBytes);
+    SpecW0* X0 = reinterpret_cast<SpecW0*>(lds + kSpecHdrBytes);
+    SpecW1* X1 = reinterpret_cast<SpecW1*>(lds + kSpecHdrBytes + kSpecW0Bytes);
+    SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes);
     const bool w0 = wave == 0;  // (wave-uniform: whose phases these are)
     int par = 0;                 // the batch's SUM buffer
-    SpecChain* X0 = reinterpret_cast<SpecChain*>(lds + kSpecHdrBytes);  // wave 0's (the views)
 
     if (!w0) {
         // Wave 1, per batch: wait for wave 0's views of the 8 proposals' configurations, then
         // the symmetry rows and the Clearance / SurfaceArea lists of every group and their
         // three ordered sums. It keeps no chain state.
-        const Staged<double> Sst{X->S[g]};
-        const Staged<float4> CLBst{X->CLB[g]};
+        const Staged<double> Sst{X1->S[g]};
+        const Staged<float4> CLBst{X1->CLB[g]};
 #pragma clang loop unroll(disable)
         for (;;) {
             const auto pv = receive_workgroup(X0->P[g], X0->RY[g], X0->XD[g], X0->YD[g]);
@@ -400,10 +419,10 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     // The current configuration's per-object and per-relationship terms (carried across
     // steps; a proposal recomputes the ones it changes).
     // (LDS shared between lanes moves through Staged / Published views, mh_common.h)
-    const Staged<ObjP> Pst{X->P[g]};
-    const Staged<double> RYst{X->RY[g]};
-    const Staged<double> Sall{&X->S[0][0]};  // every group's streams (group g at g * S_END)
-    const Staged<double> XDst{X->XD[g]}, YDst{X->YD[g]};
+    const Staged<ObjP> Pst{X0->P[g]};
+    const Staged<double> RYst{X0->RY[g]};
+    const Staged<double> Sall{&X0->S[0][0]};  // every group's streams (group g at g * S_W0)
+    const Staged<double> XDst{X0->XD[g]}, YDst{X0->YD[g]};
     const Staged<int> STOP{&SH->stop};
     if (r < n) {
         ObjP p;
@@ -422,36 +441,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     if (r + GL < nr) rel_exact(H->rel[r + GL], P0.ptr(), rpw1, rang1);
 
     // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i holds
-    // words start + i and start + 64 + i; LDS the words and the Box-Muller pairs of both.
+    // words start + i and start + 64 + i; LDS the words, the Box-Muller pairs of both, and the
+    // window's steps (StepRec) parsed once when it is filled.
     const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
-    uint64_t wbase = 0;
-    // the window: words, then the Box-Muller pairs' first and second normals
-    Pub3<unsigned int, float, float> win{{X->wd}, {X->bs}, {X->bc}};
-    auto fill = [&](uint64_t at) __attribute__((always_inline)) {
-        wbase = at;
-        const unsigned int w0 = philox_word(seed, sub, at + (uint64_t)lane);
-        const unsigned int w1 = philox_word(seed, sub, at + 64 + (uint64_t)lane);
-        // (both shuffles with every lane active, then the select: a shuffle under `lane < 63`
-        // would read lane 63 while it is inactive, and an inactive source lane reads as 0)
-        const unsigned int d0 = (unsigned int)__shfl_down((int)w0, 1);
-        const unsigned int l0 = (unsigned int)__builtin_amdgcn_readlane((int)w1, 0);
-        const unsigned int n0 = lane < 63 ? d0 : l0;
-        const unsigned int n1 = (unsigned int)__shfl_down((int)w1, 1);  // (lane 63's unused)
-        const float2 z0 = box_muller_inl(w0, n0);
-        const float2 z1 = box_muller_inl(w1, n1);
-        const auto w = restage(win);  // (every lane's reads of the previous window are done)
-        w.a.put(lane, w0);
-        w.a.put(64 + lane, w1);
-        w.b.put(lane, z0.x);
-        w.c.put(lane, z0.y);
-        w.b.put(64 + lane, z1.x);
-        w.c.put(64 + lane, z1.y);
-        win = publish(w.a, w.b, w.c);
-    };
-    fill(m0.draws);
-    unsigned int off = 0;  // next draw - window start (wave-uniform)
-    int bmh = m0.bm_has;
-    float bmv = m0.bm_val;
+    uint64_t wbase = m0.draws;
+    Pub3<unsigned int, float, float> win{{X0->wd}, {X0->bs}, {X0->bc}};
+    Published<StepRec> recv{X0->rec};
     // Draws at a lane's own offset (every lane may read a different one).
     auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
         return o < 128 ? win.a[o] : philox_far(seed, sub, wbase + o);
@@ -471,19 +466,146 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         u = u + 0.0f;
         return (int)truncf(u);
     };
-    auto pick_v = [&](unsigned int& o) __attribute__((always_inline)) {  // Kernel.cu:598-602 (index n counts as frozen)
-        int k = rand_v(o, n - 1);
-        while ((fz >> k) & 1u) k = rand_v(o, n - 1);
-        return k;
-    };
     // The Box-Muller pair (word p, word p + 1): the window's table, or computed past it.
     auto pair_v = [&](unsigned int p) __attribute__((always_inline)) -> float2 {
         if (p < 127) return make_float2(win.b[p], win.c[p]);
         return box_muller_inl(word_v(p), word_v(p + 1));
     };
+    // The mode and picks of a step starting at window offset o0 (< 124), packed with the offset
+    // after them (Kernel.cu:582, 598-602, 657-671; index n counts as frozen): mode | after << 2.
+    auto parse = [&](unsigned int o0, int& k1, int& k2) __attribute__((always_inline)) -> int {
+        const unsigned int wa = win.a[o0], wb = win.a[o0 + 1], wc = win.a[o0 + 2];
+        unsigned int o = o0 + 1;
+        const int md = rand_w(wa, 2);
+        k1 = -1;
+        k2 = -1;
+        if (md != 2 || n >= 2) {
+            k1 = rand_w(wb, n - 1);
+            o = o0 + 2;
+            while ((fz >> k1) & 1u) k1 = rand_v(o, n - 1);
+            if (md == 2) {
+                k2 = rand_w(o == o0 + 2 ? wc : word_v(o), n - 1);
+                ++o;
+                while ((fz >> k2) & 1u) k2 = rand_v(o, n - 1);
+            }
+        }
+        return md | (int)(o << 2);
+    };
+    unsigned int nrec = 0;  // steps in the window's records
+    // Fills the window at stream position `at` (the start of a step, with the Box-Muller cache
+    // (h0, bv0) before it) and parses its steps. A step's draws (Kernel.cu:576-710): the mode,
+    // the picks (with frozen redraws), the normals, Accept's uniform. Only the normals depend on
+    // the state before the step (the cached second normal h): translate takes one pair either
+    // way (h unchanged, the pair's second normal cached when h = 1), rotate one pair when h = 0
+    // (then cached) and none when h = 1, swap none. So every lane parses the steps that would
+    // start at its two offsets, a wave-uniform walk chains the window's steps (none of it
+    // depends on a decision), and lane s then writes step s's record.
+    auto fill = [&](uint64_t at, int h0, float bv0) __attribute__((always_inline)) {
+        wbase = at;
+        const unsigned int w0 = philox_word(seed, sub, at + (uint64_t)lane);
+        const unsigned int w1 = philox_word(seed, sub, at + 64 + (uint64_t)lane);
+        // (both shuffles with every lane active, then the select: a shuffle under `lane < 63`
+        // would read lane 63 while it is inactive, and an inactive source lane reads as 0)
+        const unsigned int d0 = (unsigned int)__shfl_down((int)w0, 1);
+        const unsigned int l0 = (unsigned int)__builtin_amdgcn_readlane((int)w1, 0);
+        const unsigned int n0 = lane < 63 ? d0 : l0;
+        const unsigned int n1 = (unsigned int)__shfl_down((int)w1, 1);  // (lane 63's unused)
+        const float2 z0 = box_muller_inl(w0, n0);
+        const float2 z1 = box_muller_inl(w1, n1);
+        const auto w = restage(win);  // (every lane's reads of the previous window are done)
+        w.a.put(lane, w0);
+        w.a.put(64 + lane, w1);
+        w.b.put(lane, z0.x);
+        w.c.put(lane, z0.y);
+        w.b.put(64 + lane, z1.x);
+        w.c.put(64 + lane, z1.y);
+        win = publish(w.a, w.b, w.c);
+        // the steps that would start at offsets lane and 64 + lane (past 123: not parsed)
+        int ka_lo, kb_lo, ka_hi = -1, kb_hi = -1;
+        const int pk_lo = parse((unsigned int)lane, ka_lo, kb_lo);
+        int pk_hi = 3;
+        if (lane < 60) pk_hi = parse(64u + (unsigned int)lane, ka_hi, kb_hi);
+        // the walk: (offset, h, cache position: -1 = bv0), wave-uniform; lane s keeps step s's
+        unsigned int wo = 0u, s_go = 0u, s_next = 1u;
+        int wh = __builtin_amdgcn_readfirstlane(h0), wcp = -1, s_h = 0, s_cp = -1;
+        int s = 0;
+#pragma clang loop unroll(disable)
+        for (; s < kRec && wo < 124u; ++s) {
+            const int i = __builtin_amdgcn_readfirstlane((int)wo);
+            const int vl = __builtin_amdgcn_readlane(pk_lo, i & 63);
+            const int vh = __builtin_amdgcn_readlane(pk_hi, i & 63);
+            const int v = i < 64 ? vl : vh;
+            const int md = v & 3;
+            const unsigned int pa = (unsigned int)v >> 2;
+            s_go = lane == s ? wo : s_go;
+            s_h = lane == s ? wh : s_h;
+            s_cp = lane == s ? wcp : s_cp;
+            const bool tr_ = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
+            const bool pair = tr_ || (ro && !wh);    // the step takes a Box-Muller pair
+            wcp = (tr_ && wh) || (ro && !wh) ? (int)pa : wcp;  // ... and caches its second
+            wo = pa + (pair ? 3u : 1u);
+            wh = ro ? !wh : wh;
+            s_next = lane == s ? wo : s_next;
+        }
+        nrec = (unsigned int)s;
+        // lane s: step s's record from the parsing lane, its normals and Accept's uniform
+        StepRec R;
+        {
+            const int src = (int)(s_go & 63u) << 2;
+            const bool hi = s_go >= 64u;
+            const int md_lo = __builtin_amdgcn_ds_bpermute(src, pk_lo);
+            const int md_hi = __builtin_amdgcn_ds_bpermute(src, pk_hi);
+            const int a_lo = __builtin_amdgcn_ds_bpermute(src, ka_lo);
+            const int a_hi = __builtin_amdgcn_ds_bpermute(src, ka_hi);
+            const int b_lo = __builtin_amdgcn_ds_bpermute(src, kb_lo);
+            const int b_hi = __builtin_amdgcn_ds_bpermute(src, kb_hi);
+            const int v = hi ? md_hi : md_lo;
+            R.mode = v & 3;
+            R.k1 = hi ? a_hi : a_lo;
+            R.k2 = hi ? b_hi : b_lo;
+            const unsigned int pa = (unsigned int)v >> 2;
+            const float2 z = make_float2(win.b[pa < 127 ? pa : 0], win.c[pa < 127 ? pa : 0]);
+            const float bv = s_cp < 0 ? bv0 : win.c[s_cp < 127 ? s_cp : 0];
+            const unsigned int wu = word_v(s_next - 1);
+            float zs = z.x, zc = z.y, bvi = bv;
+            if (__builtin_expect(pa >= 127 || s_cp >= 127, 0)) {  // pairs past the table
+                if (pa >= 127) {
+                    const float2 zz = pair_v(pa);
+                    zs = zz.x;
+                    zc = zz.y;
+                }
+                if (s_cp >= 127) bvi = pair_v((unsigned int)s_cp).y;
+            }
+            R.d1 = 0.0f;
+            R.d2 = 0.0f;
+            R.h = s_h;
+            R.bv = bvi;
+            if (R.mode == 0) {  // translate, Kernel.cu:595-632
+                R.d1 = (s_h ? bvi : zs) * rm.sx;
+                R.d2 = (s_h ? zs : zc) * rm.sy;
+                R.bv = zc;
+            } else if (R.mode == 1) {  // rotate, :634-653
+                const float dr = s_h ? bvi : zs;
+                R.d1 = (float)((double)dr * kSigmaT);
+                R.h = !s_h;
+                R.bv = s_h ? bvi : zc;
+            }
+            R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
+            R.next = s_next;
+            R.pad[0] = R.pad[1] = R.pad[2] = 0;
+        }
+        const Staged<StepRec> rs = restage(recv);
+        if (lane < (int)nrec) rs.put(lane, R);
+        recv = publish(rs);
+    };
+    // The stream position where the next step starts (window offset) and the cache before it.
+    unsigned int pos = 0u;
+    int pos_h = m0.bm_has;
+    float pos_bv = m0.bm_val;
+    unsigned int j0 = 0;  // records of the window consumed
+    fill(wbase, pos_h, pos_bv);
 
     unsigned int accepted = 0;
-    const float rx_sx = rm.sx, rx_sy = rm.sy;
     // The batch's tree (spec_tree), rebuilt every 32 batches from this launch's acceptance rate
     // (a prior of 2 accepts in 5 steps to start). Each lane's node is its group's.
     SpecTree tr;
@@ -509,164 +631,52 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         if ((++batches & 31u) == 0u)
             set_tree((float)(accepted + 2u) / (float)(done + 5));
-        // steps this batch can reach: the tree's depth, the launch's remaining steps
-        int kb = min(tr.maxdep + 1, a.iterations - done);
-        // At most ~5 draws per step (more only for frozen-object redraws, which then draw past
-        // the window directly): refill unless 48 remain.
-        if (off > 128 - 48) {
-            fill(wbase + off);
-            off = 0;
+        // steps this batch can reach: the tree's depth, the launch's remaining steps, the
+        // window's records (refilled at the next step's start when too few remain)
+        const int want = min(tr.maxdep + 1, a.iterations - done);
+        if ((int)(nrec - j0) < want) {
+            fill(wbase + pos, pos_h, pos_bv);
+            pos = 0u;
+            j0 = 0u;
         }
+        const int kb = min(want, (int)(nrec - j0));
         SSTAMP(0);
-        // Where each step of the batch starts in the stream. A step's draws (Kernel.cu:576-710):
-        // the mode, the picks (with frozen redraws), the normals, Accept's uniform. Only the
-        // normals depend on the state before the step (a cached second normal, h): translate
-        // takes one pair either way (h unchanged, the pair's second normal cached when h = 1),
-        // rotate one pair when h = 0 (then cached) and none when h = 1, swap none. So lane i
-        // parses the mode and picks of a step starting at off + i, and a wave-uniform walk of
-        // at most kb hops chains the batch's steps; a step starting past off + 63 (or past word
-        // 123) ends the batch early. None of this depends on a decision.
-        int pmode = 3, pk1 = -1, pk2 = -1, pafter = 0;  // (3: not parsed, the walk stops there)
-        {
-            const unsigned int o0 = off + (unsigned int)lane;
-            if (o0 < 124) {
-                const unsigned int wa = win.a[o0], wb = win.a[o0 + 1], wc = win.a[o0 + 2];
-                unsigned int o = o0 + 1;
-                pmode = rand_w(wa, 2);
-                if (pmode != 2 || n >= 2) {
-                    pk1 = rand_w(wb, n - 1);
-                    o = o0 + 2;
-                    while ((fz >> pk1) & 1u) pk1 = rand_v(o, n - 1);
-                    if (pmode == 2) {
-                        pk2 = rand_w(o == o0 + 2 ? wc : word_v(o), n - 1);
-                        ++o;
-                        while ((fz >> pk2) & 1u) pk2 = rand_v(o, n - 1);
-                    }
-                }
-                pafter = (int)o;
-            }
-        }
-        SSTAMP(8);
-        // The walk: state (o, h, cache position: -1 = the batch's incoming cached normal), all
-        // wave-uniform (readfirstlane keeps it in scalar registers), branch-free: one readlane of
-        // the packed parse per hop. Group s keeps step s's start, next start, h and cache.
-        const int pk = pmode | (pafter << 2);
-        unsigned int go = off, gnext = off + 1;
-        int gh = 0, gcp = -1;
-        const unsigned int off_s = (unsigned int)__builtin_amdgcn_readfirstlane((int)off);
-        unsigned int wo = off_s;
-        int wh = __builtin_amdgcn_readfirstlane(bmh), wcp = -1;
-        int kw = __builtin_amdgcn_readfirstlane(kb);
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-            if (s >= kw) break;
-            const int i = __builtin_amdgcn_readfirstlane((int)(wo - off_s));
-            const int v = __builtin_amdgcn_readlane(pk, i & 63);
-            const int md = i < 64 ? (v & 3) : 3;
-            kw = md == 3 ? s : kw;
-            go = g == s ? wo : go;
-            gh = g == s ? wh : gh;
-            gcp = g == s ? wcp : gcp;
-            const int pa = v >> 2;
-            const bool tr_ = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
-            const bool pair = tr_ || (ro && !wh);    // the step takes a Box-Muller pair
-            wcp = (tr_ && wh) || (ro && !wh) ? pa : wcp;  // ... and caches its second
-            wo = md == 3 ? wo : (unsigned int)pa + (pair ? 3u : 1u);
-            wh = ro ? !wh : wh;
-            gnext = g == s ? wo : gnext;
-        }
-        kb = kw;
-        if (g >= kb) {  // (groups past the batch's steps: harmless reads)
-            go = off;
-            gnext = off + 1;
-            gcp = -1;
-        }
-        SSTAMP(9);
-        // Group s's record of step s from lane (start - off)'s parse, its normals and Accept's
-        // uniform; every group then reads the records it applies by readlane (wave-uniform).
-        SpecRec R;
-        float bv_out;  // the cached second normal after the step (when h_out)
-        int h_out;
-        {
-            const int src = (int)(go - off) << 2;
-            R.mode = __builtin_amdgcn_ds_bpermute(src, pmode);
-            R.k1 = __builtin_amdgcn_ds_bpermute(src, pk1);
-            R.k2 = __builtin_amdgcn_ds_bpermute(src, pk2);
-            const unsigned int pa = (unsigned int)__builtin_amdgcn_ds_bpermute(src, pafter);
-            const float2 z = make_float2(win.b[pa < 127 ? pa : 0], win.c[pa < 127 ? pa : 0]);
-            const float bv = gcp < 0 ? bmv : win.c[gcp < 127 ? gcp : 0];
-            const unsigned int wu = word_v(gnext - 1);
-            float zs = z.x, zc = z.y, bvi = bv;
-            if (__builtin_expect(pa >= 127 || gcp >= 127, 0)) {  // pairs past the table
-                if (pa >= 127) {
-                    const float2 zz = pair_v(pa);
-                    zs = zz.x;
-                    zc = zz.y;
-                }
-                if (gcp >= 127) bvi = pair_v((unsigned int)gcp).y;
-            }
-            R.d1 = 0.0f;
-            R.d2 = 0.0f;
-            h_out = gh;
-            bv_out = bvi;
-            if (R.mode == 0) {  // translate, Kernel.cu:595-632
-                R.d1 = (gh ? bvi : zs) * rx_sx;
-                R.d2 = (gh ? zs : zc) * rx_sy;
-                bv_out = zc;
-            } else if (R.mode == 1) {  // rotate, :634-653
-                const float dr = gh ? bvi : zs;
-                R.d1 = (float)((double)dr * kSigmaT);
-                h_out = !gh;
-                bv_out = gh ? bvi : zc;
-            } else if (n < 2) {  // swap of a single object draws nothing (:657)
-                R.k1 = -1;
-                R.k2 = -1;
-            }
-            R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
-            R.live = g < kb;
-            R.pad = 0.0f;
-        }
-        SSTAMP(1);
         // Group g's configuration: the incoming state with the proposals of the steps its
         // history accepted and then its own step's applied in step order (Kernel.cu:576-704;
         // each is the reference's edit of cfgStar, made on the configuration it would see).
         double sx = cx, sy = cy, sry = cry;
         bool moved = false;  // this lane's object differs from the incoming state
-        for (int i = 0; i < kb; ++i) {  // (wave-uniform: the step's record by readlane)
+        for (int i = 0; i < kb; ++i) {  // (wave-uniform: the step's record)
             const bool app = i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
-            const int md = __builtin_amdgcn_readlane(R.mode, i << 3);
-            const int q1 = __builtin_amdgcn_readlane(R.k1, i << 3);
-            const int q2 = __builtin_amdgcn_readlane(R.k2, i << 3);
-            const float e1 = readlane_f(R.d1, i << 3);
-            if (md == 0) {  // translate
-                const float e2 = readlane_f(R.d2, i << 3);
-                if (app && r == q1) {
+            const StepRec q = recv[j0 + i];
+            if (q.mode == 0) {  // translate
+                if (app && r == q.k1) {
                     moved = true;
-                    if (sx + (double)e1 > rm.rmax_x) sx = rm.rmax_x;
-                    else if (sx + (double)e1 < rm.rmin_x) sx = rm.rmin_x;
-                    else sx = sx + (double)e1;
-                    if (sy + (double)e2 > rm.rmax_y) sy = rm.rmax_y;
-                    else if (sy + (double)e2 < rm.rmin_y) sy = rm.rmin_y;
-                    else sy = sy + (double)e2;
+                    if (sx + (double)q.d1 > rm.rmax_x) sx = rm.rmax_x;
+                    else if (sx + (double)q.d1 < rm.rmin_x) sx = rm.rmin_x;
+                    else sx = sx + (double)q.d1;
+                    if (sy + (double)q.d2 > rm.rmax_y) sy = rm.rmax_y;
+                    else if (sy + (double)q.d2 < rm.rmin_y) sy = rm.rmin_y;
+                    else sy = sy + (double)q.d2;
                 }
-            } else if (md == 1) {  // rotate
-                if (app && r == q1) {
+            } else if (q.mode == 1) {  // rotate
+                if (app && r == q.k1) {
                     moved = true;
-                    sry = sry + (double)e1;
+                    sry = sry + (double)q.d1;
                     if (sry < 0) sry = sry + kTwoPI;
                     else if (sry > kTwoPI) sry = sry - kTwoPI;
                 }
-            } else if (q1 >= 0) {  // swap (every lane active for the shuffles)
-                const int ia = gbase + q1, ib = gbase + q2;
+            } else if (q.k1 >= 0) {  // swap (every lane active for the shuffles)
+                const int ia = gbase + q.k1, ib = gbase + q.k2;
                 const double ax = shfl_d(sx, ia), ay = shfl_d(sy, ia), ary = shfl_d(sry, ia);
                 const double bx = shfl_d(sx, ib), by = shfl_d(sy, ib), bry = shfl_d(sry, ib);
                 // object 1 takes object 2's pose, object 2 object 1's through float temporaries
-                if (app && r == q2) {
+                if (app && r == q.k2) {
                     sx = (double)(float)ax;
                     sy = (double)(float)ay;
                     sry = (double)(float)ary;
                     moved = true;
-                } else if (app && r == q1) {
+                } else if (app && r == q.k1) {
                     sx = bx;
                     sy = by;
                     sry = bry;
@@ -708,7 +718,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         const uint32_t tm = (uint32_t)group_ballot<GL>(t0, gbase) |
                             ((uint32_t)group_ballot<GL>(t1, gbase) << GL);
         const int nrt = __builtin_popcount(tm), jobs = nrt + __builtin_popcount(mv);
-        const Staged<double> Sg = Sall.at(g * S_END);
+        const Staged<double> Sg = Sall.at(g * S_W0);
         if (r < n) {
             const float area = __int_as_float(H->objs[r].pad);
             Sg.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
@@ -748,8 +758,6 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         const Published<double> Sv = publish(Sall);
         SSTAMP(3);
-        SSTAMP(4);
-        SSTAMP(5);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
         // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2),
         // in the wavefront that built it (wave 1: 3, 4, 5); the workgroup barrier hands them to
@@ -765,7 +773,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 case 6: base = S_PW; len = nr; rnd = false; break;
                 default: base = S_ANG; len = nr; rnd = false; break;
             }
-            const double* src = Sv.ptr() + g * S_END + base;
+            const double* src = Sv.ptr() + g * S_W0 + base;
             double acc = 0.0;
             for (int l = 0; l < len; ++l) {
                 const double s = acc + src[l];
@@ -801,10 +809,10 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
         // total (the node whose configuration it started from, or the batch's incoming total).
-        const float u_g = shfl_f(R.u, my_dep << 3);
+        const float u_g = recv[j0 + (unsigned int)min(my_dep, kb - 1)].u;
         const float cp_tot = shfl_f(sc[0], (my_cpar == 15 ? 0 : my_cpar) << 3);
         const float cur_g = my_cpar == 15 ? cur[0] : cp_tot;
-        const bool acc_g = my_dep < kb && u_g < accept_threshold(kBeta * ((double)sc[0] - (double)cur_g));
+        const bool acc_g = my_dep < kb && accept_u(u_g, kBeta * ((double)sc[0] - (double)cur_g));
         const uint64_t ab = __ballot(acc_g && r == 0);
         // The realised path from the root: its nodes' steps commit; the configuration after
         // them is the last accepted node's (or the incoming one).
@@ -827,7 +835,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             cx = shfl_d(sx, src);
             cy = shfl_d(sy, src);
             cry = shfl_d(sry, src);
-            const double* sl = Sv.ptr() + last * S_END;
+            const double* sl = Sv.ptr() + last * S_W0;
             if (r < n) cph = (float)(-sl[S_FP + r]);
             if (r < nr) {
                 rpw0 = -sl[S_PW + r];
@@ -845,52 +853,42 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             // order: a later swap sees an earlier one's values).
             for (int d = 0; d < steps; ++d) {
                 if (!((acc_steps >> d) & 1u)) continue;
-                const int smode = __builtin_amdgcn_readlane(R.mode, d << 3);
-                const int sk1 = __builtin_amdgcn_readlane(R.k1, d << 3);
-                const int sk2 = __builtin_amdgcn_readlane(R.k2, d << 3);
-                if (smode == 2 && sk1 >= 0 && lane == 0) {
+                const StepRec q = recv[j0 + (unsigned int)d];
+                if (q.mode == 2 && q.k1 >= 0 && lane == 0) {
 #pragma unroll
                     for (int f = 0; f < 3; ++f) {
                         double* row = st + (F_Z + f) * n;
-                        const double va = row[sk1], vb = row[sk2];
-                        row[sk1] = vb;
-                        row[sk2] = (double)(float)va;
+                        const double va = row[q.k1], vb = row[q.k2];
+                        row[q.k1] = vb;
+                        row[q.k2] = (double)(float)va;
                     }
                 }
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0) {  // [done, kb, off, bmh, last, steps, cur0], per group 8 words
+        if (chain == 0 && lane == 0) {  // [done, kb, pos, j0, last, steps, cur0, nacc]
             const unsigned int base = g_spec_dbg_n;
-            if (base + 7 + 8 * K < (1u << 16)) {
-                if (lane == 0) {
-                    g_spec_dbg[base + 0] = (unsigned)done;
-                    g_spec_dbg[base + 1] = (unsigned)kb;
-                    g_spec_dbg[base + 2] = off;
-                    g_spec_dbg[base + 3] = (unsigned)bmh;
-                    g_spec_dbg[base + 4] = (unsigned)last;
-                    g_spec_dbg[base + 5] = (unsigned)steps;
-                    g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
-                }
-                if (r == 0) {
-                    unsigned int* q = g_spec_dbg + base + 7 + 8 * g;
-                    q[0] = (unsigned)R.mode;
-                    q[1] = (unsigned)R.k1;
-                    q[2] = (unsigned)R.k2;
-                    q[3] = (unsigned)R.live;
-                    q[4] = __float_as_uint(R.d1);
-                    q[5] = __float_as_uint(R.d2);
-                    q[6] = __float_as_uint(R.u);
-                    q[7] = __float_as_uint(sc[0]);
-                }
-                if (lane == 0) g_spec_dbg_n = base + 7 + 8 * K;
+            if (base + 8 < (1u << 16)) {
+                g_spec_dbg[base + 0] = (unsigned)done;
+                g_spec_dbg[base + 1] = (unsigned)kb;
+                g_spec_dbg[base + 2] = pos;
+                g_spec_dbg[base + 3] = j0;
+                g_spec_dbg[base + 4] = (unsigned)last;
+                g_spec_dbg[base + 5] = (unsigned)steps;
+                g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
+                g_spec_dbg[base + 7] = (unsigned)nacc;
+                g_spec_dbg_n = base + 8;
             }
         }
 #endif
         // The stream's state after the committed steps: what the last of them leaves.
-        off = (unsigned int)__builtin_amdgcn_readlane((int)gnext, (steps - 1) << 3);
-        bmh = __builtin_amdgcn_readlane(h_out, (steps - 1) << 3);
-        bmv = readlane_f(bv_out, (steps - 1) << 3);
+        {
+            const StepRec q = recv[j0 + (unsigned int)(steps - 1)];
+            pos = q.next;
+            pos_h = q.h;
+            pos_bv = q.bv;
+        }
+        j0 += (unsigned int)steps;
         done += steps;
         SSTAMP(7);
 #if MH_STAMPS
@@ -911,9 +909,9 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     if (lane == 0) {
         ChainMeta m = m0;
         m.accepted = m0.accepted + accepted;
-        m.draws = wbase + off;
-        m.bm_has = bmh;
-        m.bm_val = bmv;
+        m.draws = wbase + pos;
+        m.bm_has = pos_h;
+        m.bm_val = pos_bv;
 #pragma unroll
         for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
         a.meta[chain] = m;
@@ -946,9 +944,7 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsig
 }
 #endif
 
-size_t spec_lds_bytes(int waves_per_wg) {
-    return (size_t)kSpecHdrBytes + (size_t)waves_per_wg * kSpecChainBytes + kSpecSharedBytes;
-}
+size_t spec_lds_bytes(int /*waves_per_wg: always the chain's two*/) { return (size_t)kSpecBytes; }
 
 // Chains per workgroup (one: its two wavefronts share the chain), and wavefronts per chain.
 int spec_waves() { return 1; }

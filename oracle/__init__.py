@@ -228,7 +228,7 @@ def rng_streams(seed: int, subsequence: int, n: int, kind: int = PHILOX):
 
 # mh_math.h's numerics probes (MH_PROBE_*), in order
 PROBES = ["bm_log", "bm_sincos", "cos_f32", "xw_log", "xw_sincos", "atan2_room", "atan2_bits",
-          "atan2f_room", "atan2f_bits", "exp_accept", "exp_any"]
+          "atan2f_room", "atan2f_bits", "exp_accept", "exp_any", "accept"]
 
 
 def probe_width(fn: int) -> int:

@@ -981,6 +981,14 @@ static void probe_libm(int fn, uint64_t i, double* out) {
             mh_arg_atan2(i, fn == MH_PROBE_ATAN2F_BITS, &y, &x);
             out[0] = (double)(float)atan2((double)y, (double)x);
             break;
+        case MH_PROBE_ACCEPT: {
+            float u;
+            double xa;
+            mh_arg_accept(i, &u, &xa);
+            const float e = xa >= 0.0 ? 1.0f : xa < -24.0 ? 0.0f : fminf(1.0f, (float)exp(xa));
+            out[0] = u < e ? 1.0 : 0.0;
+            break;
+        }
         default: out[0] = exp(mh_arg_exp(i, fn == MH_PROBE_EXP_ANY)); break;
     }
 }

@@ -11,6 +11,9 @@ Every transcendental the chain uses is one of these probes:
 - atan2 in theta (:173), atan2f in phi (:187) and exp in Accept (:712): 2^30 sampled arguments
   each, from the distributions the chains produce (float differences of room coordinates; BETA
   (star - cur) around totals of up to 2^15) and from all float bit patterns.
+- Accept's decision itself (:712): the device decides most draws with an fp32 exp screen
+  (mh_common.h accept_u) and must return the exact decision; 2^30 (u, x) pairs, three in four
+  within 1e-4 of the threshold.
 A mismatch count is reported for each (MathReport warnings); the bar is zero.
 """
 import os
@@ -68,7 +71,8 @@ def test_exhaustive_32bit_domain(mh, orc, hiplib, probe, quarter):
     assert bad == 0, msg
 
 
-SAMPLED = ["atan2_room", "atan2_bits", "atan2f_room", "atan2f_bits", "exp_accept", "exp_any"]
+SAMPLED = ["atan2_room", "atan2_bits", "atan2f_room", "atan2f_bits", "exp_accept", "exp_any",
+           "accept"]  # (accept: the device's fp32-screened decision against the exact one)
 
 
 @pytest.mark.parametrize("probe", SAMPLED)

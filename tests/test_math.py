@@ -100,7 +100,7 @@ def test_medium_reduction_agrees_with_the_general_path(orc):
                           orc.math_apply("sin", x).view(np.uint64))
 
 
-@pytest.mark.parametrize("fn", range(11))
+@pytest.mark.parametrize("fn", range(12))
 def test_probes_are_deterministic_and_near_libm(orc, fn):
     """Each probe of the GPU check gives the same bits on any thread count, and differs from the
     C library (the oracle's math before round 4) only in the last bits: float results in at most

@@ -15,7 +15,7 @@ import __graft_entry__ as graft  # noqa: E402
 
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
-SPEC_PHASES = ["refill", "scan: group records", "apply + views", "per-object exact terms",
+SPEC_PHASES = ["refill + parse + walk + records", "", "apply + views", "per-object exact terms",
                "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
                "scan: lane parse", "scan: walk", "", ""]
 PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
