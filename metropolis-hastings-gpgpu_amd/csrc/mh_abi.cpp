@@ -303,12 +303,13 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
     g.few = plain && g.L == 64 && g.npl <= 1 && n_chains <= 8LL * cus;
     if (const char* e = getenv("MH_STEP_FEW"))
         if (*e) g.few = plain && g.L == 64 && g.npl <= 1 && atoi(e) != 0;
-    // Rooms of at most 8 objects with few chains: the speculative kernel (two wavefronts per
-    // chain) evaluates a tree of 8 proposal histories at once and commits the realised path.
-    // Measured against OP_STEP_FEW at N = 8 (chain-steps/s, profiles/r05/r05c_spec_cutoff.txt):
-    // 1,024 chains 4.56e8 / 2.6e8, 1,536 3.41e8 / 3.27e8, 1,792 3.84e8 / 3.80e8, 2,048 4.16e8 /
-    // 4.33e8 -- so up to 7 chains per CU. $MH_SPEC=0/1 forces the choice.
-    g.spec = plain && mh::spec_fits(n, c, r) && n_chains <= 7LL * cus;
+    // Rooms of at most 8 objects up to 64 chains per CU: the speculative kernel (two wavefronts
+    // per chain, 7 chains resident per CU) evaluates a tree of 8 proposal histories at once and
+    // commits the realised path. Measured against the full-evaluation kernels at N = 8
+    // (chain-steps/s, profiles/r05/r05g_*, r05h_*, r05i_*): 1,792 chains 7.56e8 / 3.78e8, 8,192
+    // 7.76e8 / 4.47e8, 16,384 8.27e8 / 7.18e8, 24,576 8.24e8 / 1.39e9, 65,536 8.52e8 / 1.64e9
+    // (the full kernel fills the GPU there). $MH_SPEC=0/1 forces the choice.
+    g.spec = plain && mh::spec_fits(n, c, r) && n_chains <= 64LL * cus;
     if (const char* e = getenv("MH_SPEC"))
         if (*e) g.spec = plain && mh::spec_fits(n, c, r) && atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);

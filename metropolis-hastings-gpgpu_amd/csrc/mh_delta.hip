@@ -114,7 +114,8 @@ struct DeltaPtrs {
     const RelConst* relg;   // HBM: the relationship records (read for the ones a move touches)
     const DevRoom* rm;
     const float *AREA, *ONES;  // replay streams shared by the workgroup
-    const double* ZERO;
+    const double* ZERO;   // 4 zero doubles
+    const float* ZEROF;   // 4 zero floats
     double *X, *Y;
     float4* BOX;  // object off-limits boxes at the current poses, zero past N
     float* RYF;   // (float)rotY
@@ -800,47 +801,52 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
 #endif
     const DevRoom& rm = *ch.rm;
     const int k = r;
+    // Each lane's three streams (multiplier, double, float); a stream a sum does not use, and
+    // every stream past its end, reads four ones or zeros that the pointer does not advance
+    // over (ch.ONES, ch.ZERO, ch.ZEROF: each typed as read).
     const float* ms = ch.ONES;
     const double* ds = ch.ZERO;
-    // the float streams as bytes: a lane past its stream's end reads the zero doubles' bytes,
-    // so its float terms are value copies (load16), never float lvalues on double storage
-    const unsigned char* fs = reinterpret_cast<const unsigned char*>(ch.ZERO);
+    const float* fs = ch.ZEROF;
+    bool dstream = false, fstream = false;
     int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
         ds = k == 0 ? ch.X : ch.Y;
+        dstream = true;
     } else if (k == 2) {
-        fs = reinterpret_cast<const unsigned char*>(ch.CPH);
+        fs = ch.CPH;
+        fstream = true;
     } else if (k == 3) {
-        fs = reinterpret_cast<const unsigned char*>(ch.NMX);
+        fs = ch.NMX;
+        fstream = true;
     } else if (k == 4) {
-        fs = reinterpret_cast<const unsigned char*>(ch.LCL);
+        fs = ch.LCL;
+        fstream = true;
     } else if (k == 5) {
-        fs = reinterpret_cast<const unsigned char*>(ch.LSA);  // (its capacity may be below NP: the stream ends at the zero-filled end)
+        fs = ch.LSA;  // (its capacity may be below NP: the stream ends at the zero-filled end)
+        fstream = true;
         lim = (min(cnt_sa, ch.cap_sa) + 3) & ~3;
     } else if (k == 6) {
         ds = ch.RPW;
+        dstream = true;
         lim = ch.NR;
     } else if (k == 7) {
         ds = ch.RANG;
+        dstream = true;
         lim = ch.NR;
     }
     double accf = 0.0, accd = 0.0;  // float- and double-accumulated walks of the same terms
     for (int l0 = 0; l0 < ch.DL; l0 += 4) {
         const bool in = l0 < lim;
-        const float* msl = in ? ms : ch.ONES;
-        const double* dsl = in ? ds : ch.ZERO;
-        const unsigned char* fsl = in ? fs : reinterpret_cast<const unsigned char*>(ch.ZERO);
-        float fv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)  // (4-byte value loads: the compiler pairs them, ds_read2_b32)
-            __builtin_memcpy(&fv[u], __builtin_assume_aligned(fsl + 4 * (l0 + u), 4), 4);
+        const float* msl = in ? ms + l0 : ch.ONES;
+        const double* dsl = in && dstream ? ds + l0 : ch.ZERO;
+        const float* fsl = in && fstream ? fs + l0 : ch.ZEROF;
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             // one rounding either way: rn(m * d) where f = 0 (VisualBalance: m = area) and
             // rn(d + f) where m = 1 (every other sum), so the fused form is the two-step one
-            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fv[u]);
+            v[u] = __builtin_fma((double)msl[u], dsl[u], (double)fsl[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];
@@ -992,10 +998,14 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         float* area = reinterpret_cast<float*>(lds + lay.h_area);
         float* ones = reinterpret_cast<float*>(lds + lay.h_ones);
         double* zero = reinterpret_cast<double*>(lds + lay.h_zero);
+        float* zerof = reinterpret_cast<float*>(lds + lay.h_zero + 32);
         for (int i = threadIdx.x; i < lay.DL; i += blockDim.x) {
             area[i] = i < n ? a.objc[i].area : 0.0f;
             ones[i] = 1.0f;
-            zero[i] = 0.0;
+        }
+        if (threadIdx.x < 4) {
+            zero[threadIdx.x] = 0.0;
+            zerof[threadIdx.x] = 0.0f;
         }
     }
     __syncthreads();
@@ -1017,6 +1027,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     ch.AREA = reinterpret_cast<const float*>(lds + lay.h_area);
     ch.ONES = reinterpret_cast<const float*>(lds + lay.h_ones);
     ch.ZERO = reinterpret_cast<const double*>(lds + lay.h_zero);
+    ch.ZEROF = reinterpret_cast<const float*>(lds + lay.h_zero + 32);
     ch.X = reinterpret_cast<double*>(base + lay.X);
     ch.Y = reinterpret_cast<double*>(base + lay.Y);
     ch.BOX = reinterpret_cast<float4*>(base + lay.BOX);

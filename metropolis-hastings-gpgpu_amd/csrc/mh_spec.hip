@@ -60,37 +60,44 @@ enum { S_VBX = 0, S_VBY = 8, S_FP = 16, S_PW = 24, S_ANG = 24 + RMAX, S_W0 = 24 
 // (:429) and the non-zero SurfaceArea terms (:463-479).
 enum { S_SYM = 0, S_CL = 8, S_SA = 8 + GL * GL, S_W1 = 8 + GL * GL + 8 * GL };
 
-// One step of the chain's stream (the draws of Kernel.cu:576-704 and Accept's, :710): a
-// chain's draws do not depend on its decisions, so a window's steps are parsed once into these
-// records and every batch reads the ones it needs.
-constexpr int kRec = 32;  // records per window
-struct StepRec {
-    int mode, k1, k2;  // the proposal (k1 = k2 = -1: a swap of a single object draws nothing)
-    int h;             // the Box-Muller cache flag after the step
-    float d1, d2;      // translate: dx, dy; rotate: the angle
-    float u;           // Accept's uniform
-    float bv;          // the cached second normal after the step (when h)
-    unsigned int next; // window offset of the next step's first draw
-    int pad[3];
+// One step of the chain's stream (the draws of Kernel.cu:576-704 and Accept's, :710). A chain's
+// draws do not depend on its decisions, so wave 1 parses the stream into these records ahead of
+// wave 0, which only reads them: a ring of kRing records, filled a window (at most kRec steps
+// of a 128-word Philox window) at a time.
+constexpr int kRec = 32;   // records per window
+constexpr int kRing = 64;  // ring entries (two windows)
+struct StepRec {  // 32 bytes (LDS per chain decides how many chains a CU holds)
+    int code;      // mode | (k1 + 1) << 2 | (k2 + 1) << 6 | h << 10: the proposal (k1 = k2 = -1:
+                   // a swap of a single object draws nothing) and the Box-Muller cache flag after it
+    float d1, d2;  // translate: dx, dy; rotate: the angle
+    float u;       // Accept's uniform
+    float bv;      // the cached second normal after the step (when h)
+    unsigned int next_lo, next_hi;  // stream position of the next step's first draw
+    int pad;
 };
+__device__ __forceinline__ int rec_mode(int code) { return code & 3; }
+__device__ __forceinline__ int rec_k1(int code) { return ((code >> 2) & 15) - 1; }
+__device__ __forceinline__ int rec_k2(int code) { return ((code >> 6) & 15) - 1; }
+__device__ __forceinline__ int rec_h(int code) { return (code >> 10) & 1; }
 
 struct SpecW0 {  // LDS of wave 0, which holds the chain
     double S[K][S_W0];            // each group's streams
     double RY[K][GL];             // each group's double rotY of every object (Symmetry, :305)
     double XD[K][GL], YD[K][GL];  // each group's double x, y (wave 1's symmetry and boxes)
     ObjP P[K][GL];                // each group's float pose words
-    unsigned int wd[128];         // the 128-word window of the Philox stream
-    float bs[128], bc[128];       // Box-Muller pairs (word i, word i + 1) of the window
-    StepRec rec[kRec];            // the window's steps
 };
 
 struct SpecW1 {  // LDS of wave 1
-    double S[K][S_W1];     // each group's streams
-    float4 CLB[K][GL];     // each group's clearance boxes at their sources (:414-415)
+    double S[K][S_W1];       // each group's streams
+    float4 CLB[K][GL];       // each group's clearance boxes at their sources (:414-415)
+    unsigned int wd[128];    // the 128-word window of the Philox stream being parsed
 };
 
 struct SpecShared {  // LDS of the chain shared by its two wavefronts
     double SUM[2][K][8];  // each group's eight sums (double-buffered by batch parity)
+    StepRec ring[kRing];  // the step records (wave 1 writes, wave 0 reads)
+    unsigned int produced;  // records written so far (wave 1; read by wave 0 between the barriers)
+    unsigned int consumed;  // records committed so far (wave 0; read by wave 1 between them)
     int stop;             // wave 0 to wave 1: the chain's steps are done
 };
 
@@ -104,8 +111,9 @@ constexpr int kSpecHdrBytes = (int)((sizeof(SpecHdr) + 15) & ~(size_t)15);
 constexpr int kSpecW0Bytes = (int)((sizeof(SpecW0) + 15) & ~(size_t)15);
 constexpr int kSpecW1Bytes = (int)((sizeof(SpecW1) + 15) & ~(size_t)15);
 constexpr int kSpecSharedBytes = (int)((sizeof(SpecShared) + 15) & ~(size_t)15);
-// (per chain: 9.7 + 9.7 + 1.0 KB and the 1.7 KB room tables, seven chains in a CU's 160 KB;
-// round 4's two full-size wave records took 37.5 KB, four chains per CU)
+// (per chain 22.1 KB with the 1.7 KB room tables: seven chains in a CU's 160 KB; round 4's two
+// full-size wave records took 37.5 KB, four chains per CU)
+static_assert(sizeof(StepRec) == 32, "StepRec");
 constexpr int kSpecBytes = kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes + kSpecSharedBytes;
 
 // A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
@@ -331,17 +339,180 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes);
     const bool w0 = wave == 0;  // (wave-uniform: whose phases these are)
     int par = 0;                 // the batch's SUM buffer
+    const ChainMeta m0 = a.meta[chain];
 
     if (!w0) {
-        // Wave 1, per batch: wait for wave 0's views of the 8 proposals' configurations, then
-        // the symmetry rows and the Clearance / SurfaceArea lists of every group and their
-        // three ordered sums. It keeps no chain state.
+        // ---- Wave 1: the stream's step records ahead of wave 0, and per batch the symmetry
+        // rows and the Clearance / SurfaceArea lists of every group. It keeps no chain state.
+        //
+        // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i
+        // holds words start + i and start + 64 + i; LDS the words and the Box-Muller pairs of
+        // both. A step's draws (Kernel.cu:576-710): the mode, the picks (with frozen redraws),
+        // the normals, Accept's uniform. Only the normals depend on the state before the step
+        // (the cached second normal h): translate takes one pair either way (h unchanged, the
+        // pair's second normal cached when h = 1), rotate one pair when h = 0 (then cached) and
+        // none when h = 1, swap none. So every lane parses the steps that would start at its two
+        // offsets of the window, a wave-uniform walk chains the window's steps (none of it
+        // depends on a decision), and lane s writes step s's record into the ring.
+        unsigned int fz = 1u << n;  // frozen flags, index n frozen (a pick of n is redrawn)
+        for (int i = 0; i < n; ++i) fz |= (a.objc[i].frozen != 0 ? 1u : 0u) << i;
+        const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
+        uint64_t wbase = 0;
+        Published<unsigned int> win{X1->wd};
+        Published<StepRec> ringv{SH->ring};
+        // Draws at a lane's own offset (every lane may read a different one).
+        auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
+            return o < 128 ? win[o] : philox_far(seed, sub, wbase + o);
+        };
+        auto rand_v = [&](unsigned int& o, int mx) __attribute__((always_inline)) {  // generateRandomIntInRange, Kernel.cu:566-574
+            float u = rocrand_device::detail::uniform_distribution(word_v(o++));
+            u = (float)((double)u * ((double)mx + 0.999999));
+            u = u + 0.0f;
+            return (int)truncf(u);
+        };
+        auto rand_w = [&](unsigned int w, int mx) __attribute__((always_inline)) {  // the same, of a word already read
+            float u = rocrand_device::detail::uniform_distribution(w);
+            u = (float)((double)u * ((double)mx + 0.999999));
+            u = u + 0.0f;
+            return (int)truncf(u);
+        };
+        // The mode and picks of a step starting at window offset o0 (< 124), packed with the
+        // offset after them (Kernel.cu:582, 598-602, 657-671; index n counts as frozen).
+        auto parse = [&](unsigned int o0, int& k1, int& k2) __attribute__((always_inline)) -> int {
+            const unsigned int wa = win[o0], wb = win[o0 + 1], wc = win[o0 + 2];
+            unsigned int o = o0 + 1;
+            const int md = rand_w(wa, 2);
+            k1 = -1;
+            k2 = -1;
+            if (md != 2 || n >= 2) {
+                k1 = rand_w(wb, n - 1);
+                o = o0 + 2;
+                while ((fz >> k1) & 1u) k1 = rand_v(o, n - 1);
+                if (md == 2) {
+                    k2 = rand_w(o == o0 + 2 ? wc : word_v(o), n - 1);
+                    ++o;
+                    while ((fz >> k2) & 1u) k2 = rand_v(o, n - 1);
+                }
+            }
+            return md | (int)(o << 2);
+        };
+        // The producer's position: where the next unparsed step starts, the cache before it.
+        uint64_t ppos = m0.draws;
+        int ph = m0.bm_has;
+        float pbv = m0.bm_val;
+        unsigned int prod = 0;  // records written
+        // One window at ppos: its words and Box-Muller pairs, its steps' records into the ring
+        // at prod, prod + 1, ...
+        auto produce = [&]() __attribute__((always_inline)) {
+            wbase = ppos;
+            const unsigned int w0 = philox_word(seed, sub, wbase + (uint64_t)lane);
+            const unsigned int w1 = philox_word(seed, sub, wbase + 64 + (uint64_t)lane);
+            const Staged<unsigned int> w = restage(win);  // (every lane's reads are done)
+            w.put(lane, w0);
+            w.put(64 + lane, w1);
+            win = publish(w);
+            // the steps that would start at offsets lane and 64 + lane (past 123: not parsed)
+            int ka_lo, kb_lo, ka_hi = -1, kb_hi = -1;
+            const int pk_lo = parse((unsigned int)lane, ka_lo, kb_lo);
+            int pk_hi = 3;
+            if (lane < 60) pk_hi = parse(64u + (unsigned int)lane, ka_hi, kb_hi);
+            // the walk: (offset, h, the step whose pair's second normal is cached: -1 = pbv),
+            // wave-uniform; lane s keeps step s's start, h, cache and next start
+            unsigned int wo = 0u, s_go = 0u, s_next = 1u;
+            int wh = __builtin_amdgcn_readfirstlane(ph), wcs = -1, s_h = 0, s_cs = -1;
+            int s = 0;
+#pragma clang loop unroll(disable)
+            for (; s < kRec && wo < 124u; ++s) {
+                const int i = __builtin_amdgcn_readfirstlane((int)wo);
+                const int vl = __builtin_amdgcn_readlane(pk_lo, i & 63);
+                const int vh = __builtin_amdgcn_readlane(pk_hi, i & 63);
+                const int v = i < 64 ? vl : vh;
+                const int md = v & 3;
+                const unsigned int pa = (unsigned int)v >> 2;
+                s_go = lane == s ? wo : s_go;
+                s_h = lane == s ? wh : s_h;
+                s_cs = lane == s ? wcs : s_cs;
+                const bool tr_ = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
+                const bool pair = tr_ || (ro && !wh);    // the step takes a Box-Muller pair
+                wcs = (tr_ && wh) || (ro && !wh) ? s : wcs;  // ... and caches its second
+                wo = pa + (pair ? 3u : 1u);
+                wh = ro ? !wh : wh;
+                s_next = lane == s ? wo : s_next;
+            }
+            const int nrec = s;
+            // lane s: step s's record from the parsing lane, its Box-Muller pair (only the steps
+            // that take one: at most one per lane), the cached normal from the step that cached
+            // it, and Accept's uniform
+            StepRec R;
+            {
+                const int src = (int)(s_go & 63u) << 2;
+                const bool hi = s_go >= 64u;
+                const int md_lo = __builtin_amdgcn_ds_bpermute(src, pk_lo);
+                const int md_hi = __builtin_amdgcn_ds_bpermute(src, pk_hi);
+                const int a_lo = __builtin_amdgcn_ds_bpermute(src, ka_lo);
+                const int a_hi = __builtin_amdgcn_ds_bpermute(src, ka_hi);
+                const int b_lo = __builtin_amdgcn_ds_bpermute(src, kb_lo);
+                const int b_hi = __builtin_amdgcn_ds_bpermute(src, kb_hi);
+                const int v = hi ? md_hi : md_lo;
+                const int mode = v & 3, k1 = hi ? a_hi : a_lo, k2 = hi ? b_hi : b_lo;
+                const unsigned int pa = (unsigned int)v >> 2;
+                const bool pair = lane < nrec && (mode == 0 || (mode == 1 && !s_h));
+                float2 z = make_float2(0.0f, 0.0f);
+                if (pair) z = box_muller_inl(word_v(pa), word_v(pa + 1));
+                const float zc_c = shfl_f(z.y, s_cs < 0 ? 0 : s_cs);  // (every lane active)
+                const float bvi = s_cs < 0 ? pbv : zc_c;
+                const unsigned int wu = word_v(s_next - 1);
+                const float zs = z.x, zc = z.y;
+                R.d1 = 0.0f;
+                R.d2 = 0.0f;
+                int h = s_h;
+                R.bv = bvi;
+                if (mode == 0) {  // translate, Kernel.cu:595-632
+                    R.d1 = (s_h ? bvi : zs) * rm.sx;
+                    R.d2 = (s_h ? zs : zc) * rm.sy;
+                    R.bv = zc;
+                } else if (mode == 1) {  // rotate, :634-653
+                    const float dr = s_h ? bvi : zs;
+                    R.d1 = (float)((double)dr * kSigmaT);
+                    h = !s_h;
+                    R.bv = s_h ? bvi : zc;
+                }
+                R.code = mode | ((k1 + 1) << 2) | ((k2 + 1) << 6) | (h << 10);
+                R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
+                const uint64_t nx = wbase + s_next;
+                R.next_lo = (unsigned int)nx;
+                R.next_hi = (unsigned int)(nx >> 32);
+                R.pad = 0;
+            }
+            const Staged<StepRec> rs = restage(ringv);
+            if (lane < nrec) rs.put((int)((prod + (unsigned int)lane) % (unsigned int)kRing), R);
+            ringv = publish(rs);
+            // the stream after the window's last step
+            const int lastl = nrec - 1;
+            ppos = ((uint64_t)(unsigned int)__builtin_amdgcn_readlane((int)R.next_hi, lastl) << 32) |
+                   (unsigned int)__builtin_amdgcn_readlane((int)R.next_lo, lastl);
+            ph = rec_h(__builtin_amdgcn_readlane(R.code, lastl));
+            pbv = readlane_f(R.bv, lastl);
+            prod += (unsigned int)nrec;
+        };
+        const Staged<unsigned int> PROD{&SH->produced};
+        produce();
+        produce();
+        if (lane == 0) PROD.put(0, prod);
+        __syncthreads();  // (wave 0 starts with these records)
+        unsigned int cons_seen = 0;  // records wave 0 had committed, as read between the barriers
         const Staged<double> Sst{X1->S[g]};
         const Staged<float4> CLBst{X1->CLB[g]};
 #pragma clang loop unroll(disable)
         for (;;) {
+            // the ring has room for a window (wave 0 reads records below cons_seen no more)
+            if (prod + (unsigned int)kRec <= cons_seen + (unsigned int)kRing) {
+                produce();
+                if (lane == 0) PROD.put(0, prod);
+            }
             const auto pv = receive_workgroup(X0->P[g], X0->RY[g], X0->XD[g], X0->YD[g]);
             if (SH->stop) break;
+            cons_seen = SH->consumed;
             const ObjP* Pg = pv.a.ptr();
             const int ro = r < n ? r : 0;
             const double sx = pv.c[ro], sy = pv.d[ro], sry = pv.b[ro];
@@ -399,19 +570,19 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         return;
     }
 
-    // Frozen flags as a mask, index n frozen (a pick of n is redrawn).
-    unsigned int fz = 1u << n;
-    for (int i = 0; i < n; ++i) fz |= (a.objc[i].frozen != 0 ? 1u : 0u) << i;
-
-    // The current configuration, in every group: lane r holds object r.
+    // ---- Wave 0: the chain ----
+    // The current configuration, in every group: lane r holds object r (z, rotX and rotZ too:
+    // no cost reads them, an accepted swap exchanges them, Kernel.cu:675-700).
     double* st = a.st + chain * (int64_t)(F_COUNT * n);
-    double cx = 0.0, cy = 0.0, cry = 0.0;
+    double cx = 0.0, cy = 0.0, cry = 0.0, cz = 0.0, crx = 0.0, crz = 0.0;
     if (r < n) {
         cx = st[F_X * n + r];
         cy = st[F_Y * n + r];
         cry = st[F_RY * n + r];
+        cz = st[F_Z * n + r];
+        crx = st[F_RX * n + r];
+        crz = st[F_RZ * n + r];
     }
-    const ChainMeta m0 = a.meta[chain];
     float cur[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) cur[k] = m0.costs[k];
@@ -424,6 +595,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     const Staged<double> Sall{&X0->S[0][0]};  // every group's streams (group g at g * S_W0)
     const Staged<double> XDst{X0->XD[g]}, YDst{X0->YD[g]};
     const Staged<int> STOP{&SH->stop};
+    const Staged<unsigned int> CONS{&SH->consumed};
     if (r < n) {
         ObjP p;
         p.xf = (float)cx;
@@ -433,6 +605,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         Pst.put(r, p);
         RYst.put(r, cry);
     }
+    if (lane == 0) CONS.put(0, 0u);
     const Published<ObjP> P0 = publish(Pst);
     float cph = 0.0f;
     double rpw0 = 0.0, rang0 = 0.0, rpw1 = 0.0, rang1 = 0.0;
@@ -440,170 +613,17 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     if (r < nr) rel_exact(H->rel[r], P0.ptr(), rpw0, rang0);
     if (r + GL < nr) rel_exact(H->rel[r + GL], P0.ptr(), rpw1, rang1);
 
-    // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i holds
-    // words start + i and start + 64 + i; LDS the words, the Box-Muller pairs of both, and the
-    // window's steps (StepRec) parsed once when it is filled.
-    const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
-    uint64_t wbase = m0.draws;
-    Pub3<unsigned int, float, float> win{{X0->wd}, {X0->bs}, {X0->bc}};
-    Published<StepRec> recv{X0->rec};
-    // Draws at a lane's own offset (every lane may read a different one).
-    auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
-        return o < 128 ? win.a[o] : philox_far(seed, sub, wbase + o);
+    __syncthreads();  // (wave 1's first records)
+    const Published<StepRec> ring{SH->ring};
+    unsigned int prod_seen = SH->produced;  // records wave 1 had written, read between barriers
+    unsigned int cons = 0;                  // records committed
+    // the stream after the last committed step (the launch's end state)
+    uint64_t end_pos = m0.draws;
+    int end_h = m0.bm_has;
+    float end_bv = m0.bm_val;
+    auto rec = [&](unsigned int i) __attribute__((always_inline)) -> const StepRec& {
+        return ring[(int)(i % (unsigned int)kRing)];
     };
-    auto uni_v = [&](unsigned int& o) __attribute__((always_inline)) {
-        return rocrand_device::detail::uniform_distribution(word_v(o++));
-    };
-    auto rand_v = [&](unsigned int& o, int mx) __attribute__((always_inline)) {  // generateRandomIntInRange, Kernel.cu:566-574
-        float u = uni_v(o);
-        u = (float)((double)u * ((double)mx + 0.999999));
-        u = u + 0.0f;
-        return (int)truncf(u);
-    };
-    auto rand_w = [&](unsigned int w, int mx) __attribute__((always_inline)) {  // the same, of a word already read
-        float u = rocrand_device::detail::uniform_distribution(w);
-        u = (float)((double)u * ((double)mx + 0.999999));
-        u = u + 0.0f;
-        return (int)truncf(u);
-    };
-    // The Box-Muller pair (word p, word p + 1): the window's table, or computed past it.
-    auto pair_v = [&](unsigned int p) __attribute__((always_inline)) -> float2 {
-        if (p < 127) return make_float2(win.b[p], win.c[p]);
-        return box_muller_inl(word_v(p), word_v(p + 1));
-    };
-    // The mode and picks of a step starting at window offset o0 (< 124), packed with the offset
-    // after them (Kernel.cu:582, 598-602, 657-671; index n counts as frozen): mode | after << 2.
-    auto parse = [&](unsigned int o0, int& k1, int& k2) __attribute__((always_inline)) -> int {
-        const unsigned int wa = win.a[o0], wb = win.a[o0 + 1], wc = win.a[o0 + 2];
-        unsigned int o = o0 + 1;
-        const int md = rand_w(wa, 2);
-        k1 = -1;
-        k2 = -1;
-        if (md != 2 || n >= 2) {
-            k1 = rand_w(wb, n - 1);
-            o = o0 + 2;
-            while ((fz >> k1) & 1u) k1 = rand_v(o, n - 1);
-            if (md == 2) {
-                k2 = rand_w(o == o0 + 2 ? wc : word_v(o), n - 1);
-                ++o;
-                while ((fz >> k2) & 1u) k2 = rand_v(o, n - 1);
-            }
-        }
-        return md | (int)(o << 2);
-    };
-    unsigned int nrec = 0;  // steps in the window's records
-    // Fills the window at stream position `at` (the start of a step, with the Box-Muller cache
-    // (h0, bv0) before it) and parses its steps. A step's draws (Kernel.cu:576-710): the mode,
-    // the picks (with frozen redraws), the normals, Accept's uniform. Only the normals depend on
-    // the state before the step (the cached second normal h): translate takes one pair either
-    // way (h unchanged, the pair's second normal cached when h = 1), rotate one pair when h = 0
-    // (then cached) and none when h = 1, swap none. So every lane parses the steps that would
-    // start at its two offsets, a wave-uniform walk chains the window's steps (none of it
-    // depends on a decision), and lane s then writes step s's record.
-    auto fill = [&](uint64_t at, int h0, float bv0) __attribute__((always_inline)) {
-        wbase = at;
-        const unsigned int w0 = philox_word(seed, sub, at + (uint64_t)lane);
-        const unsigned int w1 = philox_word(seed, sub, at + 64 + (uint64_t)lane);
-        // (both shuffles with every lane active, then the select: a shuffle under `lane < 63`
-        // would read lane 63 while it is inactive, and an inactive source lane reads as 0)
-        const unsigned int d0 = (unsigned int)__shfl_down((int)w0, 1);
-        const unsigned int l0 = (unsigned int)__builtin_amdgcn_readlane((int)w1, 0);
-        const unsigned int n0 = lane < 63 ? d0 : l0;
-        const unsigned int n1 = (unsigned int)__shfl_down((int)w1, 1);  // (lane 63's unused)
-        const float2 z0 = box_muller_inl(w0, n0);
-        const float2 z1 = box_muller_inl(w1, n1);
-        const auto w = restage(win);  // (every lane's reads of the previous window are done)
-        w.a.put(lane, w0);
-        w.a.put(64 + lane, w1);
-        w.b.put(lane, z0.x);
-        w.c.put(lane, z0.y);
-        w.b.put(64 + lane, z1.x);
-        w.c.put(64 + lane, z1.y);
-        win = publish(w.a, w.b, w.c);
-        // the steps that would start at offsets lane and 64 + lane (past 123: not parsed)
-        int ka_lo, kb_lo, ka_hi = -1, kb_hi = -1;
-        const int pk_lo = parse((unsigned int)lane, ka_lo, kb_lo);
-        int pk_hi = 3;
-        if (lane < 60) pk_hi = parse(64u + (unsigned int)lane, ka_hi, kb_hi);
-        // the walk: (offset, h, cache position: -1 = bv0), wave-uniform; lane s keeps step s's
-        unsigned int wo = 0u, s_go = 0u, s_next = 1u;
-        int wh = __builtin_amdgcn_readfirstlane(h0), wcp = -1, s_h = 0, s_cp = -1;
-        int s = 0;
-#pragma clang loop unroll(disable)
-        for (; s < kRec && wo < 124u; ++s) {
-            const int i = __builtin_amdgcn_readfirstlane((int)wo);
-            const int vl = __builtin_amdgcn_readlane(pk_lo, i & 63);
-            const int vh = __builtin_amdgcn_readlane(pk_hi, i & 63);
-            const int v = i < 64 ? vl : vh;
-            const int md = v & 3;
-            const unsigned int pa = (unsigned int)v >> 2;
-            s_go = lane == s ? wo : s_go;
-            s_h = lane == s ? wh : s_h;
-            s_cp = lane == s ? wcp : s_cp;
-            const bool tr_ = md == 0, ro = md == 1;  // translate, rotate (swap: 2)
-            const bool pair = tr_ || (ro && !wh);    // the step takes a Box-Muller pair
-            wcp = (tr_ && wh) || (ro && !wh) ? (int)pa : wcp;  // ... and caches its second
-            wo = pa + (pair ? 3u : 1u);
-            wh = ro ? !wh : wh;
-            s_next = lane == s ? wo : s_next;
-        }
-        nrec = (unsigned int)s;
-        // lane s: step s's record from the parsing lane, its normals and Accept's uniform
-        StepRec R;
-        {
-            const int src = (int)(s_go & 63u) << 2;
-            const bool hi = s_go >= 64u;
-            const int md_lo = __builtin_amdgcn_ds_bpermute(src, pk_lo);
-            const int md_hi = __builtin_amdgcn_ds_bpermute(src, pk_hi);
-            const int a_lo = __builtin_amdgcn_ds_bpermute(src, ka_lo);
-            const int a_hi = __builtin_amdgcn_ds_bpermute(src, ka_hi);
-            const int b_lo = __builtin_amdgcn_ds_bpermute(src, kb_lo);
-            const int b_hi = __builtin_amdgcn_ds_bpermute(src, kb_hi);
-            const int v = hi ? md_hi : md_lo;
-            R.mode = v & 3;
-            R.k1 = hi ? a_hi : a_lo;
-            R.k2 = hi ? b_hi : b_lo;
-            const unsigned int pa = (unsigned int)v >> 2;
-            const float2 z = make_float2(win.b[pa < 127 ? pa : 0], win.c[pa < 127 ? pa : 0]);
-            const float bv = s_cp < 0 ? bv0 : win.c[s_cp < 127 ? s_cp : 0];
-            const unsigned int wu = word_v(s_next - 1);
-            float zs = z.x, zc = z.y, bvi = bv;
-            if (__builtin_expect(pa >= 127 || s_cp >= 127, 0)) {  // pairs past the table
-                if (pa >= 127) {
-                    const float2 zz = pair_v(pa);
-                    zs = zz.x;
-                    zc = zz.y;
-                }
-                if (s_cp >= 127) bvi = pair_v((unsigned int)s_cp).y;
-            }
-            R.d1 = 0.0f;
-            R.d2 = 0.0f;
-            R.h = s_h;
-            R.bv = bvi;
-            if (R.mode == 0) {  // translate, Kernel.cu:595-632
-                R.d1 = (s_h ? bvi : zs) * rm.sx;
-                R.d2 = (s_h ? zs : zc) * rm.sy;
-                R.bv = zc;
-            } else if (R.mode == 1) {  // rotate, :634-653
-                const float dr = s_h ? bvi : zs;
-                R.d1 = (float)((double)dr * kSigmaT);
-                R.h = !s_h;
-                R.bv = s_h ? bvi : zc;
-            }
-            R.u = rocrand_device::detail::uniform_distribution(wu);  // Accept, :710
-            R.next = s_next;
-            R.pad[0] = R.pad[1] = R.pad[2] = 0;
-        }
-        const Staged<StepRec> rs = restage(recv);
-        if (lane < (int)nrec) rs.put(lane, R);
-        recv = publish(rs);
-    };
-    // The stream position where the next step starts (window offset) and the cache before it.
-    unsigned int pos = 0u;
-    int pos_h = m0.bm_has;
-    float pos_bv = m0.bm_val;
-    unsigned int j0 = 0;  // records of the window consumed
-    fill(wbase, pos_h, pos_bv);
 
     unsigned int accepted = 0;
     // The batch's tree (spec_tree), rebuilt every 32 batches from this launch's acceptance rate
@@ -632,14 +652,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         if ((++batches & 31u) == 0u)
             set_tree((float)(accepted + 2u) / (float)(done + 5));
         // steps this batch can reach: the tree's depth, the launch's remaining steps, the
-        // window's records (refilled at the next step's start when too few remain)
-        const int want = min(tr.maxdep + 1, a.iterations - done);
-        if ((int)(nrec - j0) < want) {
-            fill(wbase + pos, pos_h, pos_bv);
-            pos = 0u;
-            j0 = 0u;
-        }
-        const int kb = min(want, (int)(nrec - j0));
+        // records wave 1 has written (0: a round that only waits for it)
+        const int kb = min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
         SSTAMP(0);
         // Group g's configuration: the incoming state with the proposals of the steps its
         // history accepted and then its own step's applied in step order (Kernel.cu:576-704;
@@ -648,35 +662,38 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         bool moved = false;  // this lane's object differs from the incoming state
         for (int i = 0; i < kb; ++i) {  // (wave-uniform: the step's record)
             const bool app = i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
-            const StepRec q = recv[j0 + i];
-            if (q.mode == 0) {  // translate
-                if (app && r == q.k1) {
+            const StepRec& q = rec(cons + (unsigned int)i);
+            const int qc = q.code;
+            const int qm = rec_mode(qc), q1 = rec_k1(qc), q2 = rec_k2(qc);
+            const float qd1 = q.d1, qd2 = q.d2;
+            if (qm == 0) {  // translate
+                if (app && r == q1) {
                     moved = true;
-                    if (sx + (double)q.d1 > rm.rmax_x) sx = rm.rmax_x;
-                    else if (sx + (double)q.d1 < rm.rmin_x) sx = rm.rmin_x;
-                    else sx = sx + (double)q.d1;
-                    if (sy + (double)q.d2 > rm.rmax_y) sy = rm.rmax_y;
-                    else if (sy + (double)q.d2 < rm.rmin_y) sy = rm.rmin_y;
-                    else sy = sy + (double)q.d2;
+                    if (sx + (double)qd1 > rm.rmax_x) sx = rm.rmax_x;
+                    else if (sx + (double)qd1 < rm.rmin_x) sx = rm.rmin_x;
+                    else sx = sx + (double)qd1;
+                    if (sy + (double)qd2 > rm.rmax_y) sy = rm.rmax_y;
+                    else if (sy + (double)qd2 < rm.rmin_y) sy = rm.rmin_y;
+                    else sy = sy + (double)qd2;
                 }
-            } else if (q.mode == 1) {  // rotate
-                if (app && r == q.k1) {
+            } else if (qm == 1) {  // rotate
+                if (app && r == q1) {
                     moved = true;
-                    sry = sry + (double)q.d1;
+                    sry = sry + (double)qd1;
                     if (sry < 0) sry = sry + kTwoPI;
                     else if (sry > kTwoPI) sry = sry - kTwoPI;
                 }
-            } else if (q.k1 >= 0) {  // swap (every lane active for the shuffles)
-                const int ia = gbase + q.k1, ib = gbase + q.k2;
+            } else if (q1 >= 0) {  // swap (every lane active for the shuffles)
+                const int ia = gbase + q1, ib = gbase + q2;
                 const double ax = shfl_d(sx, ia), ay = shfl_d(sy, ia), ary = shfl_d(sry, ia);
                 const double bx = shfl_d(sx, ib), by = shfl_d(sy, ib), bry = shfl_d(sry, ib);
                 // object 1 takes object 2's pose, object 2 object 1's through float temporaries
-                if (app && r == q.k2) {
+                if (app && r == q2) {
                     sx = (double)(float)ax;
                     sy = (double)(float)ay;
                     sry = (double)(float)ary;
                     moved = true;
-                } else if (app && r == q.k1) {
+                } else if (app && r == q1) {
                     sx = bx;
                     sy = by;
                     sry = bry;
@@ -697,9 +714,11 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             YDst.put(r, sy);
         }
         if (lane == 0) STOP.put(0, 0);
+        SSTAMP(1);
         const auto pv = publish_workgroup(Pst, RYst, XDst, YDst);  // (to wave 1 as well)
         SSTAMP(2);
-        const ObjP* Pg = pv.a.ptr();
+        prod_seen = SH->produced;  // (wave 1 writes it before this barrier, never between)
+        (void)pv;  // (the views are read below through Pall: every group's)
 
         // The exact FocalPoint terms of the group's moved objects and the terms of the
         // relationships they touch, the rest carried from the incoming state. The group's
@@ -717,7 +736,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         const uint32_t tm = (uint32_t)group_ballot<GL>(t0, gbase) |
                             ((uint32_t)group_ballot<GL>(t1, gbase) << GL);
-        const int nrt = __builtin_popcount(tm), jobs = nrt + __builtin_popcount(mv);
+        const int nrt = __builtin_popcount(tm);
         const Staged<double> Sg = Sall.at(g * S_W0);
         if (r < n) {
             const float area = __int_as_float(H->objs[r].pad);
@@ -733,27 +752,52 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             Sg.put(S_PW + r + GL, -rpw1);
             Sg.put(S_ANG + r + GL, -rang1);
         }
-        for (int q = r; __ballot(q < jobs) != 0; q += GL) {  // (wave-uniform trip count)
-            const bool has = q < jobs, isrel = q < nrt;
-            const int idx = nth_bit(isrel ? tm : mv, isrel ? q : q - nrt);
+        // The 8 nodes' jobs are dealt out to the wavefront's 64 lanes (one pass unless they
+        // number more than 64): lane q takes job q of the concatenation, group by group.
+        const uint32_t jw = tm | (mv << 16) | ((uint32_t)nrt << 24);  // (group-uniform)
+        uint32_t JW[K];
+        int JP[K + 1];
+        JP[0] = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            JW[k] = (uint32_t)__builtin_amdgcn_readlane((int)jw, k << 3);
+            JP[k + 1] = JP[k] + (int)(JW[k] >> 24) + __builtin_popcount((JW[k] >> 16) & 0xffu);
+        }
+        const Published<ObjP> Pall{&X0->P[0][0]};  // (every group's view, published above)
+        for (int q0 = 0; q0 < JP[K]; q0 += 64) {  // (wave-uniform trip count)
+            const int q = q0 + lane;
+            int G = 0, base = 0;
+            uint32_t w = JW[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) {
+                const bool ge = q >= JP[k];
+                G = ge ? k : G;
+                w = ge ? JW[k] : w;
+                base = ge ? JP[k] : base;
+            }
+            const int ql = q - base, nrtG = (int)(w >> 24);
+            const bool has = q < JP[K], isrel = ql < nrtG;
+            const int idx = nth_bit(isrel ? (w & 0xffffu) : ((w >> 16) & 0xffu), isrel ? ql : ql - nrtG);
             const bool rel = has && isrel, foc = has && !isrel;
+            const ObjP* PG = Pall.ptr() + G * GL;
             const RelConst& rc = H->rel[rel ? idx : 0];
-            const ObjP qo = Pg[foc ? idx : 0];
+            const ObjP qo = PG[foc ? idx : 0];
             double ay = 0.0, ax = 1.0, pw = 0.0;
             float ti = 0.0f;
-            if (rel) pw = rel_pair(rc, Pg, ay, ax, ti);
+            if (rel) pw = rel_pair(rc, PG, ay, ax, ti);
             if (foc) {
                 ay = (double)(rm.fyf - qo.yf);
                 ax = (double)(rm.fxf - qo.xf);
             }
             const double at = atan2_ool(ay, ax);
+            const Staged<double> SG = Sall.at(G * S_W0);
             if (rel) {
-                Sg.put(S_PW + idx, -pw);
-                Sg.put(S_ANG + idx, -rel_angle(rc, at, ti));
+                SG.put(S_PW + idx, -pw);
+                SG.put(S_ANG + idx, -rel_angle(rc, at, ti));
             }
             if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
                 const float b = (float)at - qo.rotYf;
-                Sg.put(S_FP + idx, -(double)cos_f32((float)((double)b + kHalfPI)));
+                SG.put(S_FP + idx, -(double)cos_f32((float)((double)b + kHalfPI)));
             }
         }
         const Published<double> Sv = publish(Sall);
@@ -781,6 +825,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
             SUMst.put(r, acc);
         }
+        SSTAMP(4);
         const Published<double> SUMv = publish_workgroup(SUMst);
         par ^= 1;
         SSTAMP(6);
@@ -809,7 +854,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
         // total (the node whose configuration it started from, or the batch's incoming total).
-        const float u_g = recv[j0 + (unsigned int)min(my_dep, kb - 1)].u;
+        const float u_g = my_dep < kb ? rec(cons + (unsigned int)my_dep).u : 1.0f;
         const float cp_tot = shfl_f(sc[0], (my_cpar == 15 ? 0 : my_cpar) << 3);
         const float cur_g = my_cpar == 15 ? cur[0] : cp_tot;
         const bool acc_g = my_dep < kb && accept_u(u_g, kBeta * ((double)sc[0] - (double)cur_g));
@@ -849,30 +894,35 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last << 3);
             accepted += (unsigned int)nacc;
             // An accepted swap also exchanges z, rotX and rotZ (:675-700), object 1's values
-            // through float temporaries; no cost reads them, so they live in HBM only (in step
-            // order: a later swap sees an earlier one's values).
+            // through float temporaries, in step order (a later swap sees an earlier one's).
             for (int d = 0; d < steps; ++d) {
                 if (!((acc_steps >> d) & 1u)) continue;
-                const StepRec q = recv[j0 + (unsigned int)d];
-                if (q.mode == 2 && q.k1 >= 0 && lane == 0) {
-#pragma unroll
-                    for (int f = 0; f < 3; ++f) {
-                        double* row = st + (F_Z + f) * n;
-                        const double va = row[q.k1], vb = row[q.k2];
-                        row[q.k1] = vb;
-                        row[q.k2] = (double)(float)va;
+                const int qc = rec(cons + (unsigned int)d).code;
+                const int q1 = rec_k1(qc), q2 = rec_k2(qc);
+                if (rec_mode(qc) == 2 && q1 >= 0) {
+                    const int ia = gbase + q1, ib = gbase + q2;
+                    const double az = shfl_d(cz, ia), arx = shfl_d(crx, ia), arz = shfl_d(crz, ia);
+                    const double bz = shfl_d(cz, ib), brx = shfl_d(crx, ib), brz = shfl_d(crz, ib);
+                    if (r == q2) {
+                        cz = (double)(float)az;
+                        crx = (double)(float)arx;
+                        crz = (double)(float)arz;
+                    } else if (r == q1) {
+                        cz = bz;
+                        crx = brx;
+                        crz = brz;
                     }
                 }
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0 && lane == 0) {  // [done, kb, pos, j0, last, steps, cur0, nacc]
+        if (chain == 0 && lane == 0) {  // [done, kb, cons, prod_seen, last, steps, cur0, nacc]
             const unsigned int base = g_spec_dbg_n;
             if (base + 8 < (1u << 16)) {
                 g_spec_dbg[base + 0] = (unsigned)done;
                 g_spec_dbg[base + 1] = (unsigned)kb;
-                g_spec_dbg[base + 2] = pos;
-                g_spec_dbg[base + 3] = j0;
+                g_spec_dbg[base + 2] = cons;
+                g_spec_dbg[base + 3] = prod_seen;
                 g_spec_dbg[base + 4] = (unsigned)last;
                 g_spec_dbg[base + 5] = (unsigned)steps;
                 g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
@@ -881,15 +931,17 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
         }
 #endif
-        // The stream's state after the committed steps: what the last of them leaves.
-        {
-            const StepRec q = recv[j0 + (unsigned int)(steps - 1)];
-            pos = q.next;
-            pos_h = q.h;
-            pos_bv = q.bv;
+        // The stream's state after the committed steps: what the last of them leaves (read
+        // before the count is published: wave 1 may then reuse the slot).
+        if (steps > 0) {
+            const StepRec& q = rec(cons + (unsigned int)(steps - 1));
+            end_pos = ((uint64_t)q.next_hi << 32) | q.next_lo;
+            end_h = rec_h(q.code);
+            end_bv = q.bv;
         }
-        j0 += (unsigned int)steps;
+        cons += (unsigned int)steps;
         done += steps;
+        if (lane == 0) CONS.put(0, cons);  // (wave 1 reads it between the next two barriers)
         SSTAMP(7);
 #if MH_STAMPS
         cyc[14] += 1;
@@ -905,13 +957,16 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         st[F_X * n + r] = cx;
         st[F_Y * n + r] = cy;
         st[F_RY * n + r] = cry;
+        st[F_Z * n + r] = cz;
+        st[F_RX * n + r] = crx;
+        st[F_RZ * n + r] = crz;
     }
     if (lane == 0) {
         ChainMeta m = m0;
         m.accepted = m0.accepted + accepted;
-        m.draws = wbase + pos;
-        m.bm_has = pos_h;
-        m.bm_val = pos_bv;
+        m.draws = end_pos;
+        m.bm_has = end_h;
+        m.bm_val = end_bv;
 #pragma unroll
         for (int k = 0; k < 8; ++k) m.costs[k] = cur[k];
         a.meta[chain] = m;

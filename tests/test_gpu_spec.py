@@ -92,8 +92,8 @@ def test_spec_resume_split_runs(mh, hiplib, monkeypatch):
 
 
 def test_spec_is_the_default_for_few_small_chains(mh, hiplib, monkeypatch):
-    """The plain family, rooms of at most 8 objects, at most 7 chains per CU (the measured
-    crossover with the few-chains instance); MH_SPEC=0 opts out."""
+    """The plain family, rooms of at most 8 objects, at most 64 chains per CU (measured faster
+    than the full-evaluation kernels there); MH_SPEC=0 opts out."""
     monkeypatch.delenv("MH_SPEC", raising=False)
     monkeypatch.delenv("MH_DELTA", raising=False)
     with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:
@@ -102,9 +102,9 @@ def test_spec_is_the_default_for_few_small_chains(mh, hiplib, monkeypatch):
         assert s.step_kernel()[2] != "speculative"
     with mh.Session(mh.synthetic_room(16), 1024, seed=1) as s:
         assert s.step_kernel()[2] != "speculative"
-    with mh.Session(mh.synthetic_room(8), 1792, seed=1) as s:  # 7 per CU on 256 CUs
+    with mh.Session(mh.synthetic_room(8), 16384, seed=1) as s:  # 64 per CU on 256 CUs
         assert s.step_kernel()[2] == "speculative"
-    with mh.Session(mh.synthetic_room(8), 2048, seed=1) as s:
+    with mh.Session(mh.synthetic_room(8), 16385, seed=1) as s:
         assert s.step_kernel()[2] != "speculative"
     with mh.Session(mh.synthetic_room(8), 1 << 16, seed=1) as s:  # enough chains to fill the GPU
         assert s.step_kernel()[2] != "speculative"

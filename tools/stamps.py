@@ -15,9 +15,9 @@ import __graft_entry__ as graft  # noqa: E402
 
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
-SPEC_PHASES = ["refill + parse + walk + records", "", "apply + views", "per-object exact terms",
-               "store + symmetry", "CL/SA compaction", "ordered sums", "costs + accept + commit",
-               "scan: lane parse", "scan: walk", "", ""]
+SPEC_PHASES = ["tree + record count", "apply", "views barrier (wait for wave 1)",
+               "jobs (exact terms)", "own ordered sums", "", "sums barrier (wait for wave 1)",
+               "costs + accept + commit", "", "", "", ""]
 PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
           "E SA walk + CL list", "F PW/ANG + replay", "accept/undo"]
 
