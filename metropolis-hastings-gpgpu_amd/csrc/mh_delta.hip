@@ -114,7 +114,7 @@ struct DeltaPtrs {
     const RelConst* relg;   // HBM: the relationship records (read for the ones a move touches)
     const DevRoom* rm;
     const float *AREA, *ONES;  // replay streams shared by the workgroup
-    const double* ZERO;   // 4 zero doubles
+    const double* ZERO;   // double[DL] zeros
     const float* ZEROF;   // 4 zero floats
     double *X, *Y;
     float4* BOX;  // object off-limits boxes at the current poses, zero past N
@@ -773,14 +773,11 @@ __device__ __forceinline__ void save_best_delta(const DeltaPtrs& ch, const Own<S
 // entries up to round4(to) are zero (x + 0 == x).
 // The next four terms are loaded before the current four are added, so the LDS latency
 // overlaps the dependent adds (these walks run ~1,000 terms at N = 256 on few waves per SIMD).
-// (`fs`: a float list, or the replay's byte view of one)
-template <class T>
-__device__ __forceinline__ float list_walk(const T* fs, int from, int to, float a) {
+__device__ __forceinline__ float list_walk(const float* fs, int from, int to, float a) {
     if (from >= to) return a;
-    const unsigned char* b = reinterpret_cast<const unsigned char*>(fs);
-    float4 q = load16<float4>(b + 4 * from);
+    float4 q = load16<float4>(fs + from);
     for (int l = from; l < to; l += 4) {
-        const float4 nq = (l + 4 < to) ? load16<float4>(b + 4 * (l + 4)) : q;
+        const float4 nq = (l + 4 < to) ? load16<float4>(fs + l + 4) : q;
         a = a + q.x;
         a = a + q.y;
         a = a + q.z;
@@ -802,17 +799,16 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     const DevRoom& rm = *ch.rm;
     const int k = r;
     // Each lane's three streams (multiplier, double, float); a stream a sum does not use, and
-    // every stream past its end, reads four ones or zeros that the pointer does not advance
-    // over (ch.ONES, ch.ZERO, ch.ZEROF: each typed as read).
+    // every stream past its end, reads ones or zeros, each typed as read: ch.ONES and ch.ZERO (DL
+    // entries) and ch.ZEROF (four float zeros the float pointer does not advance over).
     const float* ms = ch.ONES;
     const double* ds = ch.ZERO;
     const float* fs = ch.ZEROF;
-    bool dstream = false, fstream = false;
+    bool fstream = false;
     int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
         ds = k == 0 ? ch.X : ch.Y;
-        dstream = true;
     } else if (k == 2) {
         fs = ch.CPH;
         fstream = true;
@@ -828,25 +824,23 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
         lim = (min(cnt_sa, ch.cap_sa) + 3) & ~3;
     } else if (k == 6) {
         ds = ch.RPW;
-        dstream = true;
         lim = ch.NR;
     } else if (k == 7) {
         ds = ch.RANG;
-        dstream = true;
         lim = ch.NR;
     }
     double accf = 0.0, accd = 0.0;  // float- and double-accumulated walks of the same terms
     for (int l0 = 0; l0 < ch.DL; l0 += 4) {
         const bool in = l0 < lim;
-        const float* msl = in ? ms + l0 : ch.ONES;
-        const double* dsl = in && dstream ? ds + l0 : ch.ZERO;
+        const float* msl = in ? ms : ch.ONES;
+        const double* dsl = in ? ds : ch.ZERO;
         const float* fsl = in && fstream ? fs + l0 : ch.ZEROF;
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             // one rounding either way: rn(m * d) where f = 0 (VisualBalance: m = area) and
             // rn(d + f) where m = 1 (every other sum), so the fused form is the two-step one
-            v[u] = __builtin_fma((double)msl[u], dsl[u], (double)fsl[u]);
+            v[u] = __builtin_fma((double)msl[l0 + u], dsl[l0 + u], (double)fsl[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             accd = accd + v[u];
@@ -998,15 +992,13 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         float* area = reinterpret_cast<float*>(lds + lay.h_area);
         float* ones = reinterpret_cast<float*>(lds + lay.h_ones);
         double* zero = reinterpret_cast<double*>(lds + lay.h_zero);
-        float* zerof = reinterpret_cast<float*>(lds + lay.h_zero + 32);
+        float* zerof = reinterpret_cast<float*>(lds + lay.h_zero + round16(8 * lay.DL));  // 4
         for (int i = threadIdx.x; i < lay.DL; i += blockDim.x) {
             area[i] = i < n ? a.objc[i].area : 0.0f;
             ones[i] = 1.0f;
+            zero[i] = 0.0;
         }
-        if (threadIdx.x < 4) {
-            zero[threadIdx.x] = 0.0;
-            zerof[threadIdx.x] = 0.0f;
-        }
+        if (threadIdx.x < 4) zerof[threadIdx.x] = 0.0f;
     }
     __syncthreads();
 
@@ -1027,7 +1019,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     ch.AREA = reinterpret_cast<const float*>(lds + lay.h_area);
     ch.ONES = reinterpret_cast<const float*>(lds + lay.h_ones);
     ch.ZERO = reinterpret_cast<const double*>(lds + lay.h_zero);
-    ch.ZEROF = reinterpret_cast<const float*>(lds + lay.h_zero + 32);
+    ch.ZEROF = reinterpret_cast<const float*>(lds + lay.h_zero + round16(8 * lay.DL));
     ch.X = reinterpret_cast<double*>(base + lay.X);
     ch.Y = reinterpret_cast<double*>(base + lay.Y);
     ch.BOX = reinterpret_cast<float4*>(base + lay.BOX);

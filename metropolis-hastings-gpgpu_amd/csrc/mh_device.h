@@ -185,8 +185,8 @@ inline MH_HD int bank_place(int o, unsigned* used) {
 // each ordered sum as a stream of NP = round4(N + 1) entries, zero past its end.
 struct DeltaLds {
     int hdr, h_obj, h_clr, h_rel, h_frz, h_room;
-    int h_area, h_ones, h_zero;  // float[DL] areas, float[DL] ones, 4 zero doubles then 4 zero
-                                 // floats (a stream past its end reads these, not advancing)
+    int h_area, h_ones, h_zero;  // float[DL] areas, float[DL] ones, double[DL] zeros then 4
+                                 // float zeros (each typed as the replay reads it)
     int NP;
     int NR;         // relationship stream length round4(max(R, 1))
     int DL;         // dense replay length max(NP, NR)
@@ -225,7 +225,7 @@ inline MH_HD DeltaLds make_delta_layout(int n, int c, int r) {
     l.DL = np > l.NR ? np : l.NR;
     l.h_area = h; h += round16(4 * l.DL);
     l.h_ones = h; h += round16(4 * l.DL);
-    l.h_zero = h; h += 48;
+    l.h_zero = h; h += round16(8 * l.DL) + 16;
     l.hdr = h;
     l.W = n <= 64 ? 1 : n <= 128 ? 2 : n <= 256 ? 4 : 8;  // the kernel instance's object slots
     l.SW = (c + n + 31) / 32;

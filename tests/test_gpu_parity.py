@@ -275,14 +275,20 @@ def test_full_size_config3_properties(mh, orc, hiplib):
         assert np.array_equal(costs[cid].view(np.uint32), rc[0].view(np.uint32)), cid
 
 
-@pytest.mark.parametrize("step", ["incremental", "full"])
-@pytest.mark.parametrize("n,chains,steps", [(64, 65536, 400), (20, 16384, 1500),
-                                             (256, 8192, 200), (5, 4096, 3000)])
+RUNNING_CASES = [(n, ch, st, step) for n, ch, st in [(64, 65536, 400), (20, 16384, 1500),
+                                                      (256, 8192, 200), (5, 4096, 3000)]
+                 for step in ("incremental", "full")] + [(5, 4096, 3000, "speculative"),
+                                                         (8, 16384, 2000, "speculative")]
+
+
+@pytest.mark.parametrize("n,chains,steps,step", RUNNING_CASES)
 def test_running_costs_equal_fresh_evaluation(mh, hiplib, monkeypatch, step, n, chains, steps):
     """Size-independent property of the incremental evaluation: after many accepted proposals,
     the costs every chain carries for its current state (symmetry row maxima updated
-    incrementally) equal a full re-evaluation of that state, bit for bit, on every chain."""
+    incrementally; the speculative kernel's adopted node's costs) equal a full re-evaluation of
+    that state, bit for bit, on every chain."""
     monkeypatch.setenv("MH_DELTA", "1" if step == "incremental" else "0")
+    monkeypatch.setenv("MH_SPEC", "1" if step == "speculative" else "0")
     room = mh.synthetic_room(n)
     with mh.Session(room, chains, seed=77 + n) as s:
         assert s.step_kernel()[2].split("-")[0] == step
