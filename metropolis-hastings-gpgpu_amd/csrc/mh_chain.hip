@@ -108,6 +108,8 @@ struct ChainPtrs {
     const RectShape* clrs;
     const RelConst* relc;
     const uint2* rix;  // [R] relationship i's objects {s | t << 16, as | at << 16}
+    const float4* re0;  // [R] fp32 constants of the relationships' estimates (rel_est_consts)
+    const float4* re1;
     ObjP* P;
     double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
     double *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
@@ -220,97 +222,129 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
 }
 
 // The fp32 PairWise estimate of a relationship from its objects' pose words (the reference's float
-// differences; the distance within 2 U of its double value), setting `amb` near the range's ends.
-__device__ __forceinline__ double rel_pw_est(const RelConst& rc, ObjP ps, ObjP pt, bool& amb) {
+// differences; the distance within 3 U of the reference's double), setting `amb` near the range's
+// ends. e0 = {(float)start, (float)end, 1 / start, -} (rel_est_consts); within kPwEstU U relative.
+__device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& amb) {
     constexpr float U = 0x1p-24f;
     const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;
-    const float d = __builtin_sqrtf(fx * fx + fy * fy);
-    const float st = (float)rc.start, en = (float)rc.end;
-    amb |= fabsf(d - st) <= 8.0f * U * fabsf(st) || fabsf(d - en) <= 8.0f * U * fabsf(en);
-    float f = 0.0f;
-    if (d < st) f = d / st;
-    else if (d > en) f = en / d;
+    const float d2 = fx * fx + fy * fy;
+    const float d = __builtin_amdgcn_sqrtf(d2);  // (1 ulp)
+    const float st = e0.x, en = e0.y;
+    amb |= !(d2 >= 0x1p-100f) || fabsf(d - st) <= 8.0f * U * fabsf(st) ||
+           fabsf(d - en) <= 8.0f * U * fabsf(en);
+    const float f = d < st ? d * e0.z : (d > en ? en * __builtin_amdgcn_rcpf(d) : 0.0f);
     return (double)(f * f);
 }
 
-// The fp32 PairWiseAngle estimate from theta's atan2f `tp` of (dya, dxa) and the target's pose
-// words, with its absolute allowance `eang`; `amb` near theta's wraps and the range's switch.
-__device__ __forceinline__ double rel_ang_est(const RelConst& rc, ObjP atp, float tp, float dxa,
-                                              float dya, float& eang, bool& amb) {
-    constexpr float U = 0x1p-24f;
-    amb |= fabsf(tp) <= kDeltaTh && !(dxa == 0.0f && dya == 0.0f);
-    if (tp < 0.0f) tp = tp + (float)kTwoPI;
+// The fp32 PairWiseAngle estimate from theta's estimate `tp` (atan2_est) and the target's pose
+// words, with its absolute allowance `eang`; `amb` near theta's wraps and the wrapped range's
+// switch, for a target rotation outside |rotY| < 16, or where the relationship takes no estimate.
+// e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts).
+__device__ __forceinline__ double rel_ang_est(float4 e1, float ea, ObjP atp, float tp, float& eang,
+                                              bool& amb) {
+    constexpr float U = 0x1p-24f, Y = (float)kTwoPI;
+    const int fl = __float_as_int(e1.w);
+    amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || fabsf(tp) <= kDeltaTh;
+    if (tp < 0.0f) tp = tp + Y;
     const float t = tp - atp.rotYf;
     amb |= fabsf(t) <= kDeltaTh;
-    const float th = t < 0.0f ? t + (float)kTwoPI : t;
+    const float th = t < 0.0f ? t + Y : t;
     bool on;
-    double norm;
-    if (rc.amin > rc.amax) {
-        const float w = fmodf((float)(rc.amin + (double)th), (float)kTwoPI);
-        amb |= fabsf(w - (float)rc.amax) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
-               fabsf(w - (float)kTwoPI) <= 2.0f * kDeltaTh;
-        on = (double)w > rc.amax;
-        norm = rc.norm_w;
+    if (fl & RE_WRAP) {
+        // fmodf(x, 2pi) for x in [0, 4pi) is x or x - 2pi, exact (Sterbenz); outside: exact terms
+        const float x = e1.x + th;
+        amb |= !(x >= 0.0f && x < 2.0f * Y);
+        const float w = x >= Y ? x - Y : x;
+        amb |= fabsf(w - e1.y) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
+               fabsf(w - Y) <= 2.0f * kDeltaTh;
+        on = w > e1.y;
     } else {
-        on = rc.amin < (double)th || (double)th < rc.amax;  // (continuous at its switch)
-        norm = rc.norm_n;
+        on = e1.x < th || th < e1.y;  // (continuous at its switch)
     }
-    amb |= !(fabs(norm) >= 1e-3);
-    const double v = on ? fmin(fabs((double)th - rc.amin), fabs((double)th - rc.amax)) / norm : 0.0;
-    eang = (float)((double)(2.0f * kDeltaTh) / fabs(norm)) + 4.0f * U * (float)fabs(v);
-    return v;
+    const float v = on ? fminf(fabsf(th - e1.x), fabsf(th - e1.y)) * e1.z : 0.0f;
+    eang = ea + 4.0f * U * fabsf(v);
+    return (double)v;
 }
 
-// fp32 estimates of the same terms for the rejection bound (no double transcendental): cph
-// within kDeltaCph, rpw within 12 U relative, rang within eang (returned). `amb` is set where the
-// estimate lies too near one of the reference's discontinuities for its branch to be certain --
-// the distance range's ends (:216-221), theta's two wraps (:176-181), the wrapped range's fmodf
-// and switch (:245-250) -- or the range normaliser is degenerate; such a lane needs exact_terms().
+// fp32 estimates of the same terms for the rejection bound (no double arithmetic, no division,
+// no library transcendental): cph within kDeltaCph, rpw within kPwEstU U relative, rang within
+// eang (returned). `amb` (relationship) / `ambo` (object) are set where the estimate lies too
+// near one of the reference's discontinuities for its branch to be certain -- the distance
+// range's ends (:216-221), theta's two wraps (:176-181), the wrapped range's fmodf and switch
+// (:245-250) -- or outside the ranges the allowances are derived for (mh_common.h kDeltaCph);
+// such a lane needs exact_terms(). Relationship i's objects come from rix[i] (16-bit indices).
+__device__ __forceinline__ void rel_objs(const ChainPtrs& ch, int i, ObjP& ps, ObjP& pt, ObjP& as,
+                                         ObjP& atp) {
+    const uint2 q = ch.rix[i];
+    ps = ch.P[q.x & 0xffffu];
+    pt = ch.P[q.x >> 16];
+    as = ch.P[q.y & 0xffffu];
+    atp = ch.P[q.y >> 16];
+}
+
+// the focal term's estimate from the focal angle's estimate `at` (Kernel.cu:271, 277)
+__device__ __forceinline__ float cph_est(float at, ObjP p, bool& ambo) {
+    const float ph = (at - p.rotYf) + (float)kHalfPI;
+    ambo |= !(fabsf(p.rotYf) < 16.0f) || !(fabsf(ph) < 16.0f);
+    return cos_est(ph);
+}
+
 template <bool SHARE>
 __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,
                                              bool obj, bool rel, float& cph, double& rpw,
-                                             double& rang, float& eang, bool& amb) {
+                                             double& rang, float& eang, bool& amb, bool& ambo) {
+    constexpr float TINY = 0x1p-100f;  // (atan2_est's domain)
     if constexpr (!SHARE) {
         // (the latency-bound few-chains instance: two passes, the object's first -- 4.20
         // against 4.24 ms per config-2 launch with the shared pass)
         if (obj) {
             const ObjP p = ch.P[i < n ? i : 0];
-            const float at = atan2f(rm.fyf - p.yf, rm.fxf - p.xf);
-            const float b = at - p.rotYf;
-            cph = cosf(b + (float)kHalfPI);
+            const float fy = rm.fyf - p.yf, fx = rm.fxf - p.xf;
+            ambo |= !(fmaxf(fabsf(fy), fabsf(fx)) >= TINY);
+            cph = cph_est(atan2_est(fy, fx), p, ambo);
         }
         if (rel) {
-            const RelConst& rc = ch.relc[i];
-            const ObjP ps = ch.P[rc.s], pt = ch.P[rc.t];
-            const ObjP as = ch.P[rc.as], atp = ch.P[rc.at];
-            rpw = rel_pw_est(rc, ps, pt, amb);
-            rang = rel_ang_est(rc, atp, atan2f(as.yf - atp.yf, as.xf - atp.xf),
-                               as.xf - atp.xf, as.yf - atp.yf, eang, amb);
+            ObjP ps, pt, as, atp;
+            rel_objs(ch, i, ps, pt, as, atp);
+            const float4 e0 = ch.re0[i], e1 = ch.re1[i];
+            rpw = rel_pw_est(e0, ps, pt, amb);
+            const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
+            amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= TINY);
+            rang = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), eang, amb);
         }
         return;
     }
-    // One atan2f pass serves a relationship lane's angle (theta) or, failing that, an object
+    // One atan2 pass serves a relationship lane's angle (theta) or, failing that, an object
     // lane's focal angle; a lane needing both (its object moved and its relationship was touched)
     // takes a second pass (config 3: 115.2 -> 114.4 ms per launch).
     const ObjP p = ch.P[i < n ? i : 0];
     const float fy = rm.fyf - p.yf, fx = rm.fxf - p.xf;
     float ay = fy, ax = fx;
-    const RelConst* rc = nullptr;
+    float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
     ObjP atp;
     if (rel) {
-        rc = &ch.relc[i];
-        const ObjP ps = ch.P[rc->s], pt = ch.P[rc->t];
-        rpw = rel_pw_est(*rc, ps, pt, amb);
-        const ObjP as = ch.P[rc->as];
-        atp = ch.P[rc->at];
+        ObjP ps, pt, as;
+        rel_objs(ch, i, ps, pt, as, atp);
+        e0 = ch.re0[i];
+        e1 = ch.re1[i];
+        rpw = rel_pw_est(e0, ps, pt, amb);
         ay = as.yf - atp.yf;
         ax = as.xf - atp.xf;
     }
-    const float a1 = atan2f(ay, ax);
+    const bool tiny = !(fmaxf(fabsf(ay), fabsf(ax)) >= TINY);
+    const float a1 = atan2_est(ay, ax);
     float at = a1;
-    if (obj && rel) at = atan2f(fy, fx);
-    if (obj) cph = cosf((at - p.rotYf) + (float)kHalfPI);
-    if (rel) rang = rel_ang_est(*rc, atp, a1, ax, ay, eang, amb);
+    if (obj && rel) {
+        at = atan2_est(fy, fx);
+        ambo |= !(fmaxf(fabsf(fy), fabsf(fx)) >= TINY);
+    } else if (obj) {
+        ambo |= tiny;
+    }
+    if (obj) cph = cph_est(at, p, ambo);
+    if (rel) {
+        amb |= tiny;
+        rang = rel_ang_est(e1, e0.w, atp, a1, eang, amb);
+    }
 }
 
 // ---- incremental Clearance pairs (one object per lane) ---------------------------------------
@@ -447,18 +481,19 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             clo.dr = clp.dr;
             clo.eang = clp.eang;
             if constexpr (FAST) {
-                bool amb = false;
+                bool amb = false, ambo = false;
                 if (__ballot(moved || touched))
                     approx_terms<!PAIRS>(ch, rm, i, n, moved, touched, cph[m], rpw[m], rang[m], clo.eang,
-                                 amb);
+                                 amb, ambo);
                 clo.dc = clo.dc || moved;
                 clo.dr = clo.dr || touched;
-                if (__ballot(amb)) {  // (rare) an estimate near a discontinuity: exact instead
+                if (__ballot(amb || ambo)) {  // (rare) an estimate near a discontinuity: exact
                     if (amb) {
                         clo.dr = false;
                         clo.eang = 0.0f;
                     }
-                    exact_terms(ch, rm, i, n, false, amb, cph[m], rpw[m], rang[m]);
+                    if (ambo) clo.dc = false;
+                    exact_terms(ch, rm, i, n, ambo, amb, cph[m], rpw[m], rang[m]);
                 }
             } else {
                 const bool obj = moved || (i < n && clp.dc);
@@ -914,7 +949,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             bt.pwd = bt.angd = 0.0;
             bt.efp = r < n && clo.dc ? kDeltaCph : 0.0f;  // (fp32 estimates, approx_terms)
             bt.eang = r < rm.r && clo.dr ? clo.eang : 0.0f;
-            bt.pwx = __ballot(r < rm.r && clo.dr) ? 12 : 0;
+            bt.pwx = __ballot(r < rm.r && clo.dr) ? kPwEstU : 0;
             bt.sa = -((sac[0].x + sac[0].y + sac[0].z + sac[0].w) +
                       (sao[0].x + sao[0].y + sao[0].z + sao[0].w));
             bt.pw = -(float)rpw[0];
@@ -967,7 +1002,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                 // the estimates' allowances, against the exact values
                 MH_CK(!obj || fabsf(cph[0] - c0) <= kDeltaCph, 30, __float_as_uint(cph[0]),
                       __float_as_uint(c0));
-                MH_CK(!rel || fabs(rpw[0] - p0) <= 12.0 * 0x1p-24 * fabs(p0) + 1e-30, 31,
+                MH_CK(!rel || fabs(rpw[0] - p0) <= kPwEstU * 0x1p-24 * fabs(p0) + 1e-30, 31,
                       __float_as_uint((float)rpw[0]), __float_as_uint((float)p0));
                 MH_CK(!rel || fabs(rang[0] - a0) <= (double)clo.eang, 32,
                       __float_as_uint((float)rang[0]), __float_as_uint((float)a0));
@@ -1479,11 +1514,14 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         clrs_l[i] = s;
     }
     uint2* rix_l = reinterpret_cast<uint2*>(lds + a.lay.h_rix);
+    float4* re0_l = reinterpret_cast<float4*>(lds + a.lay.h_re);
+    float4* re1_l = re0_l + (a.rm.r > 0 ? a.rm.r : 1);
     for (int i = threadIdx.x; i < a.rm.r; i += blockDim.x) {
         const RelConst rc = a.relc[i];
         relc_l[i] = rc;
         rix_l[i] = make_uint2((unsigned)rc.s | ((unsigned)rc.t << 16),
                               (unsigned)rc.as | ((unsigned)rc.at << 16));
+        rel_est_consts(rc, re0_l[i], re1_l[i]);
     }
     for (int i = threadIdx.x; i <= n; i += blockDim.x) frozen[i] = (i < n) ? (a.objc[i].frozen != 0) : 1;
     DevRoom* rm_l = reinterpret_cast<DevRoom*>(lds + F.h_room);
@@ -1504,6 +1542,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.clrs = clrs_l;
     ch.relc = relc_l;
     ch.rix = rix_l;
+    ch.re0 = re0_l;
+    ch.re1 = re1_l;
     ch.P = reinterpret_cast<ObjP*>(base + F.P);
     ch.PX = reinterpret_cast<double*>(base + F.PX);
     ch.PY = reinterpret_cast<double*>(base + F.PY);

@@ -1161,11 +1161,86 @@ struct ClPairs {
 
 // Allowances of the fp32 estimates of the FocalPoint and relationship terms (mh_chain.hip
 // approx_terms): |cos(phi) estimate - the reference's float| <= kDeltaCph, theta's estimate
-// within kDeltaTh of the reference's double, the PairWise term within 12 U relative. The
-// derivation assumes fp32 atan2 and cos within 4 ulp (OCML's are within 2-3); the check build
-// verifies every estimate against the exact value.
+// within kDeltaTh of the reference's double, the PairWise term within kPwEstU U relative. The
+// check build verifies every estimate against the exact value (sites 30-32).
+//   theta: atan2_est within 2^-20 (below), the wrap's + 2pi and the rotation's subtraction each
+//   rounded at |values| < 32 (the callers require |rotY| < 16): 3 x 2^-20 more, so 2^-18 in all.
+//   cos(phi): the angle as above plus the reference's own float roundings of at, b and phi
+//   (|phi| < 16: 2^-20 each), cos_est within 2^-22: under 2^-17.4.
+//   PairWise: the distance within 3 U (float squares and sum, a 1-ulp square root), 1 / start
+//   and (float) end within U each, the products U each, the hardware reciprocal 2 U: f within
+//   7 U, f * f within 15 U + O(U^2).
 constexpr float kDeltaCph = 0x1p-17f;
 constexpr float kDeltaTh = 0x1p-17f;
+constexpr int kPwEstU = 20;
+
+// atan2(y, x) in fp32 for the rejection bound's estimates: the octant reduction t = min / max
+// (hardware reciprocal, 1 ulp), an odd degree-15 polynomial fitted to atan on [0, 1] (2^-23 in
+// fp32 Horner form), then pi/2 - a, pi - a and y's sign. Within 2^-21.3 of atan2 over 4e7
+// random and near-diagonal pairs (numpy emulation with the reciprocal 1 ulp off either way), so
+// 2^-20 is the figure the allowances use. Requires max(|x|, |y|) >= 2^-100 (callers check: a
+// zero vector or a denormal maximum would meet the reciprocal's flush).
+__device__ __forceinline__ float atan2_est(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float t = mn * __builtin_amdgcn_rcpf(mx);
+    const float s = t * t;
+    float p = -0.0040545351803302765f;
+    p = __builtin_fmaf(p, s, 0.021862849593162537f);
+    p = __builtin_fmaf(p, s, -0.05591217800974846f);
+    p = __builtin_fmaf(p, s, 0.09642186760902405f);
+    p = __builtin_fmaf(p, s, -0.1390862613916397f);
+    p = __builtin_fmaf(p, s, 0.19946564733982086f);
+    p = __builtin_fmaf(p, s, -0.33329859375953674f);
+    p = __builtin_fmaf(p, s, 0.9999993443489075f);
+    float a = p * t;
+    a = ay > ax ? 1.5707963705062866f - a : a;
+    a = x < 0.0f ? 3.1415927410125732f - a : a;
+    return __builtin_copysignf(a, y);
+}
+
+// cos(x) in fp32 for |x| < 16 (callers check): x - k pi/2 by a two-constant fused reduction
+// (within 2^-24), sin / cos polynomials fitted on [-pi/4, pi/4] (2^-24 in fp32), the quadrant's
+// sign and choice. Within 2^-22 of cos(x).
+__device__ __forceinline__ float cos_est(float x) {
+    const float k = __builtin_rintf(x * 0.63661977236758134f);
+    float r = __builtin_fmaf(-k, 1.5707963705062866f, x);
+    r = __builtin_fmaf(-k, -4.37113882867379e-08f, r);
+    const float s = r * r;
+    const float ps = __builtin_fmaf(__builtin_fmaf(s, -0.00019488755788188428f,
+                                                   0.008331923745572567f), s, -0.16666649281978607f);
+    const float sn = __builtin_fmaf(r * s, ps, r);
+    const float pc = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(s, 2.438225783407688e-05f,
+                                                                  -0.0013886678498238325f),
+                                                   s, 0.04166661947965622f),
+                                    s, -0.5f);
+    const float cs = __builtin_fmaf(s, pc, 1.0f);
+    const int q = (int)k;
+    const float v = (q & 1) ? sn : cs;
+    return ((q + 1) & 2) ? -v : v;
+}
+
+// The fp32 constants of relationship i's estimates, staged with the room tables (two float4
+// per relationship, each array read one record per lane):
+//   e0 = {(float)start, (float)end, 1 / start, the angle allowance's constant part}
+//   e1 = {(float)amin, (float)amax, 1 / norm of the range (wrapped or plain), flags}
+// flags: bit 0 the range wraps (amin > amax, Kernel.cu:245); bit 1 no estimate (the term is
+// always evaluated exactly): a degenerate normaliser (|norm| < 1e-3), |amin| or |amax| >= 64, or
+// a non-finite constant. The angle allowance: theta within kDeltaTh, amin / amax rounded to
+// float (U |a| <= kDeltaTh / 2 for |a| < 64) and the subtraction, min and product roundings (3 U
+// |v|): 2 kDeltaTh |1 / norm| + 4 U |v| covers them; e0.w is the first part rounded up.
+enum { RE_WRAP = 1, RE_EXACT = 2 };
+__device__ __forceinline__ void rel_est_consts(const RelConst& rc, float4& e0, float4& e1) {
+    const bool wrap = rc.amin > rc.amax;
+    const double norm = wrap ? rc.norm_w : rc.norm_n;
+    const bool ok = fabs(norm) >= 1e-3 && fabs(rc.amin) < 64.0 && fabs(rc.amax) < 64.0 &&
+                    fabs(rc.start) < 1e30 && fabs(rc.end) < 1e30 && rc.start != 0.0;
+    const float inv_st = ok ? (float)(1.0 / rc.start) : 0.0f;
+    const float ea = ok ? (float)(2.0 * (double)kDeltaTh / fabs(norm) * (1.0 + 0x1p-20)) : 0.0f;
+    e0 = make_float4((float)rc.start, (float)rc.end, inv_st, ea);
+    e1 = make_float4((float)rc.amin, (float)rc.amax, ok ? (float)(1.0 / norm) : 0.0f,
+                     __int_as_float((wrap ? RE_WRAP : 0) | (ok ? 0 : RE_EXACT)));
+}
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
 // Split form for callers that batch the atan2: rel_pair() gives the PairWise term and theta's

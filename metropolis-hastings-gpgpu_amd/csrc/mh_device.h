@@ -146,6 +146,7 @@ struct ChainLds {
     int h_rix;   // uint2[R] the relationships' objects {s | t << 16, as | at << 16}: the step's
                  // per-lane "does the move touch relationship i" test reads these 8-byte words
                  // (the 64-byte RelConst stride put all 32 lanes on two banks)
+    int h_re;    // float4[2][R] the relationships' fp32 estimate constants (rel_est_consts)
     int h_frz;   // unsigned char[N + 1] frozen flags (index N counts as frozen)
     int h_room;  // DevRoom copy (read by the out-of-line cost evaluation)
     int P;       // ObjP[N]   {float xf, yf, rotYf, pad} (the double x, y, rotY live in the
@@ -321,6 +322,7 @@ inline MH_HD ChainLds make_lds_layout(int n, int c, int r, int L, bool with_off 
     int h = f.h_clr + round16((int)sizeof(RectShape) * (c > 0 ? c : 1));
     l.h_rel = h;  h += round16((int)sizeof(RelConst) * (r > 0 ? r : 1));
     l.h_rix = h;  h += round16(8 * (r > 0 ? r : 1));
+    l.h_re = h;   h += 32 * (r > 0 ? r : 1);
     l.hdr = h;
     l.P = f.P;
     l.AUX = f.AUX;
