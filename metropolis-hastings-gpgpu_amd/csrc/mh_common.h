@@ -1055,9 +1055,11 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     // magnitudes (alin, for the catch-all term) rides along in sum[7] with the angle terms'
     // magnitudes when their sum is fp64 (DPW: sum[7] then only scales a 2^-53 error), in sum[6]
     // otherwise
+    // (eang / cr32 from the hardware reciprocal, 1 ulp, raised by 8 U: never below the quotient)
+    const float icr = __builtin_amdgcn_rcpf(cr32) * (1.0f + 8.0f * U);
     const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin,
                            bt.anx + bt.any + (DPW ? 0.0f : alin),
-                           bt.aang + (DPW ? alin : bt.eang / cr32)};
+                           bt.aang + (DPW ? alin : bt.eang * icr)};
     float sum[8];
     wave_fsum8(part, sum);
     const float s_nx = sum[0], s_ny = sum[1], s_lin = sum[4], s_elin = sum[5];
@@ -1067,18 +1069,22 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const float id = fabsf(rm.inv_denom);
     const float cv = (n + 26.0f + kf) * U;  // (float accumulators, Kernel.cu:200-201)
     // The chain of the reference's roundings below -- (enx + eny) = S for the two sums, 3 U on
-    // ad, bd (the division), 2 U on fx, fy (the centroid subtraction), 2 U on the distance, 3 U
+    // ad, bd (the division), 2 U on fx, fy (the centroid subtraction), 3 U on the distance (the
+    // reference's correctly rounded root, U, and this estimate's 1-ulp hardware root, 2 U), 3 U
     // on the weight product -- composed with each (1 + kU) factor expanded: the exact error of
-    // w_vb vb is at most |w_vb| (S (1 + 11 U) + 3.01 U A + 2.01 U F + 6 U |vb|), A = |ad| + |bd|,
+    // w_vb vb is at most |w_vb| (S (1 + 12 U) + 3.01 U A + 2.01 U F + 7 U |vb|), A = |ad| + |bd|,
     // F = |fx| + |fy|; written with 32 U, 4 U, 4 U and 8 U to absorb this expression's own roundings.
     const float S = cv * id * (a_nx + a_ny);
     const float ad = s_nx * rm.inv_denom, bd = s_ny * rm.inv_denom;
     const float fx = ad - rm.cxf, fy = bd - rm.cyf;
-    const float vb = -__builtin_sqrtf(fx * fx + fy * fy);
+    const float vb = -__builtin_amdgcn_sqrtf(fx * fx + fy * fy);
     const float o2 = rm.w_vb * vb;
+    // (+ 2^-40: a root of a denormal argument, where the hardware root's 1 ulp is not promised,
+    // is below 2^-60)
     const float e2 = fabsf(rm.w_vb) *
                      (S * (1.0f + 32.0f * U) +
-                      4.0f * U * ((fabsf(ad) + fabsf(bd)) + (fabsf(fx) + fabsf(fy)) + 2.0f * fabsf(vb)));
+                      4.0f * U * ((fabsf(ad) + fabsf(bd)) + (fabsf(fx) + fabsf(fy)) + 2.0f * fabsf(vb)) +
+                      0x1p-40f);
     // PairWise x PairWiseAngle (Kernel.cu:518), both sums accumulated in double (:222, :249-253)
     float pa, dpa;
     if constexpr (DPW) {
