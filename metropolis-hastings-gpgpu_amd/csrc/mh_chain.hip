@@ -61,6 +61,8 @@ struct ChainAux {
     int nb;       // backups in use (0, 1 or 2)
     int swap_a, swap_b;  // a swap proposal's objects (-1: none); z/rotX/rotZ swap in HBM on accept
     float cur[8]; // resultCosts of the current configuration
+    float star[8];  // resultCosts of the proposal, when exact (the step keeps only its total in a
+                    // register: held across the rare exact current pass, the eight spilled)
     uint64_t rng_key[3];  // the Philox stream's seed and subsequence, the window's first draw
                           // (WaveRngLds::ss)
 #if MH_STAMPS
@@ -429,7 +431,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
                            CostIv cur = CostIv{0.0f, 0.0f}, int* fast = nullptr,
-                           CostIv* star_iv = nullptr) {
+                           CostIv* star_iv = nullptr, float* save = nullptr) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
     // (the few-chains instance reads them from the kernel arguments: no LDS round trip on its
@@ -443,7 +445,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // lane keep terms across steps and share one atan2 pass (below); the 8-lane instance (rooms
     // of up to 8 objects: latency-bound, few chains) keeps the direct per-lane passes.
     constexpr bool SHARED = DELTA && NPL == 1 && L >= 16;
-    double px[NPL], py[NPL];
+    float px[NPL], py[NPL];  // the VisualBalance products rounded to float (the bound's terms)
     float cph[NPL], rxs[NPL], rys[NPL], rrs[NPL];
     float4 sao[NPL], sac[NPL];
     float4 boxo[NPL];  // each owned object's box at its pose (SurfaceArea, Clearance pairs)
@@ -454,7 +456,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
-        px[m] = py[m] = 0.0;
+        px[m] = py[m] = 0.0f;
         cph[m] = rxs[m] = rys[m] = rrs[m] = 0.0f;
         rpw[m] = rang[m] = 0.0;
         sao[m] = sac[m] = boxo[m] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -510,8 +512,13 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             const double x = op.x[m], y = op.y[m];
             wild |= !(fabs(x) < 1e15 && fabs(y) < 1e15 && fabs(op.ry[m]) < 1e15);
             // VisualBalanceCosts products, Kernel.cu:200-201.
-            px[m] = (double)area * x;
-            py[m] = (double)area * y;
+            // (to the replay's LDS streams at once: held in registers to the replay, the
+            // doubles spilled on the exact paths)
+            const double vx = (double)area * x, vy = (double)area * y;
+            ch.PX[i] = vx;
+            ch.PY[i] = vy;
+            px[m] = (float)vx;
+            py[m] = (float)vy;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
             // object per lane: above, sharing the relationship terms' atan2 pass).
             if (!(MH_ABLATE & 2) && !SHARED) {
@@ -902,10 +909,10 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
 #if MH_DOUBLE & 256
             for (int rep = 0; rep < 2; ++rep) {
             MH_CLOBBER();
-            double px0 = px[0];
+            float px0 = px[0];
             asm volatile("" : "+v"(px0));  // (the probe's second pass is not folded into the first)
 #else
-            const double px0 = px[0];
+            const float px0 = px[0];
 #endif
             float clsum = clp.clc;
             uint64_t bits = r < n ? clo.cm : 0ull;
@@ -934,8 +941,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             }
 #endif
             BoundTerms bt;
-            bt.nx = (float)px0;
-            bt.ny = (float)py[0];
+            bt.nx = px0;
+            bt.ny = py[0];
             bt.anx = fabsf(bt.nx);
             bt.any = fabsf(bt.ny);
             bt.fp = -cph[0];
@@ -1032,8 +1039,6 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
         if (i < n) {
-            ch.PX[i] = px[m];
-            ch.PY[i] = py[m];
             ch.CPHF[i] = -cph[m];
             ch.RMXF[i] = -sym.mx[m];
         }
@@ -1272,6 +1277,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     t = t + out[5];
     t = t + out[7];
     out[0] = t;
+    if (save && r == 0)  // (the caller then keeps only the total in a register)
+        for (int k = 0; k < 8; ++k) save[k] = out[k];
 }
 
 // ---- propose(), Kernel.cu:566-704, applied in place --------------------------------------
@@ -1678,7 +1685,9 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             if constexpr (FASTK) u_acc = rng.uniform();
             eval_costs<L, NPL, false, true, FASTK, OP == OP_STEP_FEW>(
                 a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y, cls, cl, u_acc, cur_iv, &fast,
-                &star_iv);
+                &star_iv, ch.aux->star);
+            // (exact costs only; a scalar register where the chain owns the wavefront)
+            const float star0 = fast != BOUND_OPEN ? 0.0f : L == 64 ? uniform_f(sc[0]) : sc[0];
             MH_STAMP(ts);
 #if MH_CHECK
             if constexpr (FASTK)
@@ -1686,7 +1695,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             // Check builds verify every decision the bound takes against the exact costs: the
             // proposal's exact total lies in the bound's interval, the current total in the
             // carried one, and a certain REJECT / ACCEPT is Accept's decision.
-            float chk_star = sc[0];
+            float chk_star = star0;
             if constexpr (FASTK) {
                 if (fast != BOUND_OPEN) {
                     float cx[8];
@@ -1720,12 +1729,12 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 // alone (decide_exact_star); only otherwise is the current configuration made
                 // exact.
                 if (__builtin_expect(fast == BOUND_OPEN && !cur_exact, 0)) {
-                    const int d2 = decide_exact_star(sc[0], cur_iv, u_acc, kBeta);
+                    const int d2 = decide_exact_star(star0, cur_iv, u_acc, kBeta);
 #if MH_CHECK
                     if (r == 0 && d2 != BOUND_OPEN) {
                         const bool acc_x = u_acc < accept_threshold(
-                                               kBeta * ((double)sc[0] - (double)chk_cur));
-                        MH_CK(acc_x == (d2 == BOUND_ACCEPT), 25, __float_as_uint(sc[0]),
+                                               kBeta * ((double)star0 - (double)chk_cur));
+                        MH_CK(acc_x == (d2 == BOUND_ACCEPT), 25, __float_as_uint(star0),
                               __float_as_uint(chk_cur));
                     }
 #endif
@@ -1768,7 +1777,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     }
 #endif
                     wave_sync();
-                    if (u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total))) {
+                    if (u_acc < accept_threshold(kBeta * ((double)star0 - (double)cur_total))) {
                         restore<L, NPL>(ch, op, r, writer, kk);  // the proposal again
                         fast = BOUND_ACCEPT + 1;  // accepted with exact costs (below)
                     } else {
@@ -1779,22 +1788,22 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             }
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
             if constexpr (TRACK) {
-                if (a.track != TRACK_OFF && best_improves(a.track, sc[0], best_total)) {
-                    best_total = sc[0];
+                if (a.track != TRACK_OFF && best_improves(a.track, star0, best_total)) {
+                    best_total = star0;
                     save_best_pose<L, NPL>(ch, op, a.best + chain * (int64_t)(F_COUNT * n), n, r);
                 }
             }
             bool acc;
             bool exact = true;  // accepted with its exact costs
-            if constexpr (TRACK) acc = accept_at(rng, sc[0], cur_total, beta);
+            if constexpr (TRACK) acc = accept_at(rng, star0, cur_total, beta);
             else if constexpr (FASTK) {
                 if (fast == BOUND_OPEN)
-                    acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
+                    acc = u_acc < accept_threshold(kBeta * ((double)star0 - (double)cur_total));
                 else
                     acc = fast == BOUND_ACCEPT || fast == BOUND_ACCEPT + 1 ||
                           fast == BOUND_ACCEPT + 32;
                 exact = fast != BOUND_ACCEPT;
-            } else acc = accept(rng, sc[0], cur_total);
+            } else acc = accept(rng, star0, cur_total);
             if (acc) {
                 sym = ss;
                 cl = cls;
@@ -1803,7 +1812,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 if constexpr (FASTK) chk_cur = chk_star;
 #endif
                 if (exact) {
-                    cur_total = sc[0];
+                    cur_total = star0;
                     if constexpr (FASTK) {
                         cur_exact = true;
                         cur_iv = CostIv{cur_total, cur_total};
@@ -1814,7 +1823,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 }
                 if (writer) {
                     if (exact)
-                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = sc[k];
+                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = ch.aux->star[k];
                     commit_swap_zrr(ch, n);
                 }
             } else if (fast != BOUND_REJECT + 16) {

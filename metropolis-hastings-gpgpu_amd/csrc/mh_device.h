@@ -130,9 +130,9 @@ __device__ __forceinline__ void save_best(const Ptrs& ch, double* dst, int n, in
 
 // Per-chain scalars of the full-evaluation kernel (mh_chain.hip ChainAux), bytes.
 #if defined(MH_STAMPS) && MH_STAMPS
-constexpr int kChainAuxBytes = 240;
+constexpr int kChainAuxBytes = 272;
 #else
-constexpr int kChainAuxBytes = 144;
+constexpr int kChainAuxBytes = 176;
 #endif
 
 // LDS carve-up of the full-evaluation kernel. One workgroup = WAVES waves; each wave holds
