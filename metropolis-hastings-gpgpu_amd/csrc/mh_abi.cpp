@@ -593,6 +593,9 @@ bool session_finalize(mh_session* s, hipStream_t st) {
     return record_done(s, st);
 }
 
+// Downloads below this size never page-lock the caller's buffer.
+constexpr size_t kLockMinBytes = 1u << 20;
+
 // $MH_DOWNLOAD_PAGEABLE=1: downloads never page-lock the caller's buffer (the staged copy only,
 // for the A/B of the two).
 bool download_pageable() {
@@ -609,7 +612,15 @@ bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes, bool loc
     if (bytes == 0) return true;
     hipStream_t st = s->stream;
     if (!order_after_last(s, st)) return false;
-    const bool locked = !locked_by_caller && !download_pageable() &&
+    // The session's kernels first, so that a failure is attributed to them and not to the copy.
+    if (const hipError_t ek = hipStreamSynchronize(st); ek != hipSuccess) {
+        set_error(std::string("the session's kernels failed before the download: ") +
+                  hipGetErrorString(ek));
+        return false;
+    }
+    // Small results take the runtime's staged copy: page-locking a few unaligned pages of the
+    // caller's heap per call buys nothing there.
+    const bool locked = !locked_by_caller && !download_pageable() && bytes >= kLockMinBytes &&
                         hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
     if (!locked) (void)hipGetLastError();  // (clear the sticky error of the failed lock)
     MH_TRY_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));

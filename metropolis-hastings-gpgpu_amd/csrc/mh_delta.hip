@@ -427,10 +427,25 @@ __device__ __forceinline__ bool clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
     return chg0;
 }
 
+// The relationship terms a proposal overwrote, so that an undo swaps them back instead of
+// evaluating them again (a double atan2, a root and two divisions per relationship): up to two
+// per lane (a move touches a handful of relationships), each with its slot t (relationship
+// t * L + r). A swap, so a second undo re-applies the proposal's terms (the rare exact pass of
+// the current configuration). A lane with more touched relationships sets `all`: the undo then
+// evaluates them again.
+struct RelBk {
+    double pw[2], ang[2];
+    int slot[2];
+    int cnt;
+    bool all;
+};
+
 // PairWise / PairWiseAngle terms of the relationships touching ka or kb (or all, ka = -2).
 // The hit test reads the relationship objects from LDS; the records themselves (ranges,
-// normalisers) come from HBM, for the few relationships a move touches.
-__device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r) {
+// normalisers) come from HBM, for the few relationships a move touches. `bk`: the overwritten
+// terms are kept there (the proposal's update).
+__device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r,
+                                           RelBk* bk = nullptr) {
     uint64_t pend = 0;
     int t = 0;
     for (int q = r; q < nr; q += L, ++t) {
@@ -441,14 +456,54 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
                          (kb >= 0 && (s0 == kb || t0 == kb || s1 == kb || t1 == kb));
         if (hit) pend |= 1ull << t;
     }
+    if (bk) {
+        bk->cnt = 0;
+        bk->all = __builtin_popcountll(pend) > 2;
+    }
     while (__ballot(pend != 0)) {
         if (pend) {
-            const int q = __builtin_ctzll(pend) * L + r;
+            const int u = __builtin_ctzll(pend);
+            const int q = u * L + r;
             pend &= pend - 1;
+            if (bk && bk->cnt < 2) {
+                const int k = bk->cnt;
+                const double p = ch.RPW[q], g = ch.RANG[q];
+                if (k == 0) {  // (constant indices: registers, not scratch)
+                    bk->pw[0] = p;
+                    bk->ang[0] = g;
+                    bk->slot[0] = u;
+                } else {
+                    bk->pw[1] = p;
+                    bk->ang[1] = g;
+                    bk->slot[1] = u;
+                }
+                bk->cnt = k + 1;
+            }
             double tpw, tang;
             rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
             ch.RPW[q] = -tpw;
             ch.RANG[q] = -tang;
+        }
+    }
+}
+
+// Undo of rels_delta's proposal update: the kept terms swapped back (or, where a lane's record
+// is incomplete, the touched relationships evaluated again).
+__device__ __forceinline__ void rels_undo(const DeltaPtrs& ch, int nr, int ka, int kb, int r,
+                                          RelBk& bk) {
+    if (__ballot(bk.all)) {
+        rels_delta(ch, nr, ka, kb, r);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k < bk.cnt) {
+            const int q = bk.slot[k] * L + r;
+            const double p = ch.RPW[q], g = ch.RANG[q];
+            ch.RPW[q] = bk.pw[k];
+            ch.RANG[q] = bk.ang[k];
+            bk.pw[k] = p;
+            bk.ang[k] = g;
         }
     }
 }
@@ -940,7 +995,7 @@ __device__ __forceinline__ void replay_config(const DeltaPtrs& ch, const typenam
 // pair bits, the relationship terms.
 template <int S>
 __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, int n, int c, int nr,
-                                              int ka, int kb, int r, bool writer) {
+                                              int ka, int kb, int r, bool writer, RelBk& rbk) {
     const int nb = ch.aux->nb;
     for (int q = nb - 1; q >= 0; --q) {
         const DBackup b = ch.aux->b[q];
@@ -954,7 +1009,7 @@ __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, in
     }
     wave_sync();
     clearance_delta<S>(ch, o, n, c, ka, kb, r);
-    rels_delta(ch, nr, ka, kb, r);
+    rels_undo(ch, nr, ka, kb, r, rbk);
     wave_sync();
 }
 
@@ -1182,7 +1237,8 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         DSTAMP(0);
         const bool chg0 = clearance_delta<S>(ch, o, n, c, ka, kb, r);
         DSTAMP(1);
-        rels_delta(ch, nr, ka, kb, r);
+        RelBk rbk;
+        rels_delta(ch, nr, ka, kb, r, &rbk);
         DSTAMP(2);
         symmetry_delta<S>(ch, o, n, ka, kb, wild_star > 0, r);
         wave_sync();
@@ -1363,7 +1419,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             const int nb = ch.aux->nb;
             const DBackup p0 = read_obj<S>(ch, o, nb > 0 ? ch.aux->b[0].k : 0);
             const DBackup p1 = read_obj<S>(ch, o, nb > 1 ? ch.aux->b[1].k : 0);
-            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer);
+            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk);
             if (writer) {
                 if (nb > 0) ch.aux->b[0] = p0;
                 if (nb > 1) ch.aux->b[1] = p1;
@@ -1393,7 +1449,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         else acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
         // A rejected proposal is undone; after the exact pass of the current configuration
         // (rare) the state is the current one, and an accepted proposal is re-applied.
-        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer);
+        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk);
         if (acc) {
             ++accepted;
 #if MH_CHECK
