@@ -153,7 +153,8 @@ __device__ __forceinline__ float4 cla_box(const DeltaPtrs& ch, int ci) {
 // Clearance ci's box: its owner lane's register (ci < 64) or LDS. `own`: this lane owns ci.
 template <int S>
 __device__ __forceinline__ float4 cla_get(const DeltaPtrs& ch, const Own<S>& o, int ci) {
-    return ci < 64 ? o.cla0 : ch.CLA[ci - 64];
+    if (ci < 64) return o.cla0;  // (not a ?: of the two lvalues: a select of their addresses
+    return ch.CLA[ci - 64];      // put the register copy in scratch)
 }
 template <int S>
 __device__ __forceinline__ void cla_put(const DeltaPtrs& ch, Own<S>& o, int ci, float4 v) {
@@ -406,9 +407,14 @@ __device__ __forceinline__ bool clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
             if (rows & (1ull << t)) continue;
             const bool nz = overlap(cla_get<S>(ch, o, ci), bj) != 0.0f;
             if (t == 0) {
-                const uint64_t w0 = o.nz0[j >> 6];
+                const int wj = j >> 6;  // (selects: no dynamic register indexing)
+                uint64_t w0 = 0;
+#pragma unroll
+                for (int q = 0; q < S; ++q) w0 = q == wj ? o.nz0[q] : w0;
                 chg0 = chg0 || nz || (w0 & bit) != 0;
-                o.nz0[j >> 6] = nz ? (w0 | bit) : (w0 & ~bit);
+                const uint64_t w1 = nz ? (w0 | bit) : (w0 & ~bit);
+#pragma unroll
+                for (int q = 0; q < S; ++q) o.nz0[q] = q == wj ? w1 : o.nz0[q];
             } else {
                 uint64_t* wd = &ch.NZ[(ci - 64) * S + (j >> 6)];
                 *wd = nz ? (*wd | bit) : (*wd & ~bit);
@@ -995,7 +1001,8 @@ __device__ __forceinline__ void replay_config(const DeltaPtrs& ch, const typenam
 // pair bits, the relationship terms.
 template <int S>
 __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, int n, int c, int nr,
-                                              int ka, int kb, int r, bool writer, RelBk& rbk) {
+                                              int ka, int kb, int r, bool writer, RelBk& rbk,
+                                              typename Own<S>::wvec& bk_nz) {
     const int nb = ch.aux->nb;
     for (int q = nb - 1; q >= 0; --q) {
         const DBackup b = ch.aux->b[q];
@@ -1008,7 +1015,20 @@ __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, in
         ch.SAMB[w] = t;
     }
     wave_sync();
-    clearance_delta<S>(ch, o, n, c, ka, kb, r);
+    // The Clearance row words the proposal overwrote in registers (clearances < 64) are swapped
+    // back, not recomputed (a swap: a second undo re-applies the proposal's), and a clearance
+    // whose source moved takes its box at the restored pose; rooms of more than 64 clearances,
+    // whose further rows live in LDS, recompute.
+    if (c <= 64) {
+        const typename Own<S>::wvec w = o.nz0;
+        o.nz0 = bk_nz;
+        bk_nz = w;
+        const bool moved = r < c && (ch.clrs[r].pad == ka || ch.clrs[r].pad == kb);
+        if (__ballot(moved))
+            if (moved) o.cla0 = cla_box(ch, r);
+    } else {
+        clearance_delta<S>(ch, o, n, c, ka, kb, r);
+    }
     rels_undo(ch, nr, ka, kb, r, rbk);
     wave_sync();
 }
@@ -1235,6 +1255,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         const int wild_star = wild_cnt + __shfl(dwild, 0) + __shfl(dwild, 1);
         wave_sync();
         DSTAMP(0);
+        typename Own<S>::wvec bk_nz = o.nz0;  // (the undo's record, undo_proposal)
         const bool chg0 = clearance_delta<S>(ch, o, n, c, ka, kb, r);
         DSTAMP(1);
         RelBk rbk;
@@ -1419,7 +1440,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             const int nb = ch.aux->nb;
             const DBackup p0 = read_obj<S>(ch, o, nb > 0 ? ch.aux->b[0].k : 0);
             const DBackup p1 = read_obj<S>(ch, o, nb > 1 ? ch.aux->b[1].k : 0);
-            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk);
+            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz);
             if (writer) {
                 if (nb > 0) ch.aux->b[0] = p0;
                 if (nb > 1) ch.aux->b[1] = p1;
@@ -1449,7 +1470,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         else acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
         // A rejected proposal is undone; after the exact pass of the current configuration
         // (rare) the state is the current one, and an accepted proposal is re-applied.
-        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk);
+        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz);
         if (acc) {
             ++accepted;
 #if MH_CHECK
