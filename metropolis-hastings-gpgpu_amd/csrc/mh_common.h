@@ -782,12 +782,25 @@ template <int L>
 __device__ __forceinline__ SymLead group_sym_lead(float t1, float t2, int tj, int r, int gbase,
                                                   float rr) {
     float m = t1;
-    m = fmaxf(m, bfly<1>(m));
-    m = fmaxf(m, bfly<2>(m));
-    if constexpr (L >= 8) m = fmaxf(m, bfly<4>(m));
-    if constexpr (L >= 16) m = fmaxf(m, bfly<8>(m));
-    if constexpr (L >= 32) m = fmaxf(m, bfly<16>(m));
-    if constexpr (L >= 64) m = fmaxf(m, bfly<32>(m));
+    if constexpr (L == 64) {
+        // (one chain per wavefront: the row maxima by DPP, then row_bcast15 / row_bcast31 carry
+        // them into lane 63, read as a scalar -- as wave_fsum, with -inf where a row is not
+        // written; no permlane swaps)
+        constexpr int NEG_INF = (int)0xff800000u;
+        m = fmaxf(m, __int_as_float(dpp_mov<0xB1>(__float_as_int(m))));   // quad_perm [1,0,3,2]
+        m = fmaxf(m, __int_as_float(dpp_mov<0x4E>(__float_as_int(m))));   // quad_perm [2,3,0,1]
+        m = fmaxf(m, __int_as_float(dpp_mov<0x141>(__float_as_int(m))));  // row_half_mirror
+        m = fmaxf(m, __int_as_float(dpp_mov<0x140>(__float_as_int(m))));  // row_mirror
+        m = fmaxf(m, __int_as_float(dpp_mov<0x142, 0xA, 0xF, false>(__float_as_int(m), NEG_INF)));
+        m = fmaxf(m, __int_as_float(dpp_mov<0x143, 0xC, 0xF, false>(__float_as_int(m), NEG_INF)));
+        m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 63));
+    } else {
+        m = fmaxf(m, bfly<1>(m));
+        m = fmaxf(m, bfly<2>(m));
+        if constexpr (L >= 8) m = fmaxf(m, bfly<4>(m));
+        if constexpr (L >= 16) m = fmaxf(m, bfly<8>(m));
+        if constexpr (L >= 32) m = fmaxf(m, bfly<16>(m));
+    }
     // t1 is never NaN (it only takes values that compare greater), so some lane holds m.
     const uint64_t at = group_ballot<L>(t1 == m, gbase);
     const int lb = __builtin_ctzll(at);
