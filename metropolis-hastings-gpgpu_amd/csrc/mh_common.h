@@ -941,17 +941,27 @@ __device__ __forceinline__ double bfly_add(double v) {
     return v + __hiloint2double(bfly<OFF>(__double2hiint(v)), bfly<OFF>(__double2loint(v)));
 }
 
-// Sum of a double over the 64 lanes of the wavefront, uniform: six butterfly levels, six fp64
-// additions per lane in a fixed order (error <= 6 * 2^-53 * sum |v| beyond the lanes' own).
+// One DPP level of a double: v + (the DPP source lane's v), both halves moved by dpp_mov (rows
+// the row mask leaves out add 0).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_add(double v) {
+    return v + __hiloint2double(dpp_mov<CTRL, ROW_MASK, 0xF, false>(__double2hiint(v), 0),
+                                dpp_mov<CTRL, ROW_MASK, 0xF, false>(__double2loint(v), 0));
+}
+
+// Sum of a double over the 64 lanes of the wavefront, uniform: the row sums by DPP (quad_perm,
+// row_half_mirror, row_mirror), then row_bcast15 / row_bcast31 carry them into lane 63 -- six
+// fp64 additions in a fixed order on the way to lane 63 (error <= 6 * 2^-53 * sum |v| beyond the
+// lanes' own), as wave_fsum; no permlane swaps.
 __device__ __forceinline__ double wave_dsum(double v) {
-    v = bfly_add<1>(v);
-    v = bfly_add<2>(v);
-    v = bfly_add<4>(v);
-    v = bfly_add<8>(v);
-    v = bfly_add<16>(v);
-    v = bfly_add<32>(v);
-    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+    v = dpp_add<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v = dpp_add<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v = dpp_add<0x141>(v);  // row_half_mirror
+    v = dpp_add<0x140>(v);  // row_mirror
+    v = dpp_add<0x142, 0xA>(v);  // row_bcast15 into rows 1 and 3
+    v = dpp_add<0x143, 0xC>(v);  // row_bcast31 into rows 2 and 3
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                            __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
 // Sum of v over the 64 lanes of the wavefront, uniform (an SGPR): in-row butterflies (DPP
