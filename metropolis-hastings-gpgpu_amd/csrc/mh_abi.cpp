@@ -54,6 +54,7 @@ struct Room {
     std::vector<mh::ObjConst> obj;
     std::vector<mh::ClrConst> clr;
     std::vector<mh::RelConst> rel;
+    std::vector<float4> rele;  // [2][R] (mh::rel_est_consts)
     std::vector<double> cfg0;  // [6][N]
 };
 
@@ -205,6 +206,9 @@ bool build_room(const relationshipStruct* rss, const relationshipAngleStruct* rs
         r.norm_w = (mh::kTwoPI - (r.amax + (mh::kTwoPI - r.amin))) / 2.0;
         r.norm_n = (mh::kTwoPI - (r.amax - r.amin)) / 2.0;
     }
+    out.rele.assign(2 * out.rel.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+    for (size_t i = 0; i < out.rel.size(); ++i)
+        mh::rel_est_consts(out.rel[i], out.rele[i], out.rele[out.rel.size() + i]);
     out.cfg0.resize((size_t)mh::F_COUNT * n);
     for (int i = 0; i < n; ++i) {
         out.cfg0[mh::F_X * n + i] = cfg[i].x;
@@ -390,6 +394,7 @@ struct mh_session {
     mh::ObjConst* d_obj = nullptr;
     mh::ClrConst* d_clr = nullptr;
     mh::RelConst* d_rel = nullptr;
+    float4* d_rele = nullptr;
     double* d_cfg0 = nullptr;
     double* d_st = nullptr;
     double* d_best = nullptr;  // [n_chains][6][N] best-of-chain configurations (track on)
@@ -399,7 +404,7 @@ struct mh_session {
     mh_summary* d_summary = nullptr;
     // Element capacities of the buffers above: a pooled session (KernelWrapper's cache) keeps
     // its buffers across calls and grows one only when a call needs more.
-    size_t cap_obj = 0, cap_clr = 0, cap_rel = 0, cap_cfg0 = 0, cap_st = 0, cap_best = 0,
+    size_t cap_obj = 0, cap_clr = 0, cap_rel = 0, cap_rele = 0, cap_cfg0 = 0, cap_st = 0, cap_best = 0,
            cap_xw = 0, cap_ladder = 0, cap_perm = 0, cap_meta = 0, cap_pts = 0, cap_costs = 0,
            cap_summary = 0;
     // The geometry's inputs (choose_geometry runs only when they change)
@@ -420,6 +425,7 @@ struct mh_session {
         a.objc = d_obj;
         a.clrc = d_clr;
         a.relc = d_rel;
+        a.rele = d_rele;
         a.cfg = d_cfg0;
         a.st = d_st;
         a.meta = d_meta;
@@ -454,6 +460,7 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_obj);
     (void)hipFree(s->d_clr);
     (void)hipFree(s->d_rel);
+    (void)hipFree(s->d_rele);
     (void)hipFree(s->d_cfg0);
     (void)hipFree(s->d_st);
     (void)hipFree(s->d_best);
@@ -533,6 +540,7 @@ bool session_init(mh_session* s) {
     if (!upload(&s->d_obj, s->cap_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->cap_clr, s->room.clr, s->stream)) return false;
     if (!upload(&s->d_rel, s->cap_rel, s->room.rel, s->stream)) return false;
+    if (!upload(&s->d_rele, s->cap_rele, s->room.rele, s->stream)) return false;
     if (!upload(&s->d_cfg0, s->cap_cfg0, s->room.cfg0, s->stream)) return false;
     const int64_t nc = s->n_chains > 0 ? s->n_chains : 1;
     const size_t n = (size_t)s->room.rm.n;

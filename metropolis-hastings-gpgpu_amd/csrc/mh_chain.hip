@@ -223,50 +223,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     }
 }
 
-// The fp32 PairWise estimate of a relationship from its objects' pose words (the reference's float
-// differences; the distance within 3 U of the reference's double), setting `amb` near the range's
-// ends. e0 = {(float)start, (float)end, 1 / start, -} (rel_est_consts); within kPwEstU U relative.
-__device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& amb) {
-    constexpr float U = 0x1p-24f;
-    const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;
-    const float d2 = fx * fx + fy * fy;
-    const float d = __builtin_amdgcn_sqrtf(d2);  // (1 ulp)
-    const float st = e0.x, en = e0.y;
-    amb |= !(d2 >= 0x1p-100f) || fabsf(d - st) <= 8.0f * U * fabsf(st) ||
-           fabsf(d - en) <= 8.0f * U * fabsf(en);
-    const float f = d < st ? d * e0.z : (d > en ? en * __builtin_amdgcn_rcpf(d) : 0.0f);
-    return (double)(f * f);
-}
-
-// The fp32 PairWiseAngle estimate from theta's estimate `tp` (atan2_est) and the target's pose
-// words, with its absolute allowance `eang`; `amb` near theta's wraps and the wrapped range's
-// switch, for a target rotation outside |rotY| < 16, or where the relationship takes no estimate.
-// e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts).
-__device__ __forceinline__ double rel_ang_est(float4 e1, float ea, ObjP atp, float tp, float& eang,
-                                              bool& amb) {
-    constexpr float U = 0x1p-24f, Y = (float)kTwoPI;
-    const int fl = __float_as_int(e1.w);
-    amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || fabsf(tp) <= kDeltaTh;
-    if (tp < 0.0f) tp = tp + Y;
-    const float t = tp - atp.rotYf;
-    amb |= fabsf(t) <= kDeltaTh;
-    const float th = t < 0.0f ? t + Y : t;
-    bool on;
-    if (fl & RE_WRAP) {
-        // fmodf(x, 2pi) for x in [0, 4pi) is x or x - 2pi, exact (Sterbenz); outside: exact terms
-        const float x = e1.x + th;
-        amb |= !(x >= 0.0f && x < 2.0f * Y);
-        const float w = x >= Y ? x - Y : x;
-        amb |= fabsf(w - e1.y) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
-               fabsf(w - Y) <= 2.0f * kDeltaTh;
-        on = w > e1.y;
-    } else {
-        on = e1.x < th || th < e1.y;  // (continuous at its switch)
-    }
-    const float v = on ? fminf(fabsf(th - e1.x), fabsf(th - e1.y)) * e1.z : 0.0f;
-    eang = ea + 4.0f * U * fabsf(v);
-    return (double)v;
-}
+// (rel_pw_est, rel_ang_est: mh_common.h, shared with the incremental kernel)
 
 // fp32 estimates of the same terms for the rejection bound (no double arithmetic, no division,
 // no library transcendental): cph within kDeltaCph, rpw within kPwEstU U relative, rang within
@@ -284,12 +241,7 @@ __device__ __forceinline__ void rel_objs(const ChainPtrs& ch, int i, ObjP& ps, O
     atp = ch.P[q.y >> 16];
 }
 
-// the focal term's estimate from the focal angle's estimate `at` (Kernel.cu:271, 277)
-__device__ __forceinline__ float cph_est(float at, ObjP p, bool& ambo) {
-    const float ph = (at - p.rotYf) + (float)kHalfPI;
-    ambo |= !(fabsf(p.rotYf) < 16.0f) || !(fabsf(ph) < 16.0f);
-    return cos_est(ph);
-}
+// (cph_est: mh_common.h)
 
 template <bool SHARE>
 __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom& rm, int i, int n,

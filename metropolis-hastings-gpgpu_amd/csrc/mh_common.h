@@ -1117,8 +1117,14 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
         const double spw = wave_dsum(bt.pwd), sang = wave_dsum(bt.angd);
         const double pad = spw * sang;
         const float cr = (float)((double)(nrel + bt.k + 12) * 0x1p-53);
-        const float epw = cr * (float)fabs(spw) * (1.0f + 64.0f * U),
-                    eang = cr * a_ang * (1.0f + 64.0f * U);
+        float epw = cr * (float)fabs(spw) * (1.0f + 64.0f * U),
+              eang = cr * a_ang * (1.0f + 64.0f * U);
+        if (bt.pwx) {  // (uniform) estimated relationship terms (the incremental kernel's
+                       // EstState): kPwEstU U relative on PairWise, eang each on the angles; the
+                       // fp32 tree sum of the allowances raised by 8 U, 64 U on the relative part
+            epw += (float)bt.pwx * U * (float)fabs(spw) * (1.0f + 64.0f * U);
+            eang += wave_fsum(bt.eang) * (1.0f + 8.0f * U);
+        }
         pa = (float)pad;
         dpa = (float)fabs(spw) * eang + (float)fabs(sang) * epw + epw * eang +
               (float)(0x1p-52 * fabs(pad));
@@ -1199,9 +1205,7 @@ struct ClPairs {
 //   PairWise: the distance within 3 U (float squares and sum, a 1-ulp square root), 1 / start
 //   and (float) end within U each, the products U each, the hardware reciprocal 2 U: f within
 //   7 U, f * f within 15 U + O(U^2).
-constexpr float kDeltaCph = 0x1p-17f;
-constexpr float kDeltaTh = 0x1p-17f;
-constexpr int kPwEstU = 20;
+// (kDeltaCph, kDeltaTh, kPwEstU: mh_device.h, shared with the host's estimate constants)
 
 // atan2(y, x) in fp32 for the rejection bound's estimates: the octant reduction t = min / max
 // (hardware reciprocal, 1 ulp), an odd degree-15 polynomial fitted to atan on [0, 1] (2^-23 in
@@ -1249,27 +1253,60 @@ __device__ __forceinline__ float cos_est(float x) {
     return ((q + 1) & 2) ? -v : v;
 }
 
-// The fp32 constants of relationship i's estimates, staged with the room tables (two float4
-// per relationship, each array read one record per lane):
-//   e0 = {(float)start, (float)end, 1 / start, the angle allowance's constant part}
-//   e1 = {(float)amin, (float)amax, 1 / norm of the range (wrapped or plain), flags}
-// flags: bit 0 the range wraps (amin > amax, Kernel.cu:245); bit 1 no estimate (the term is
-// always evaluated exactly): a degenerate normaliser (|norm| < 1e-3), |amin| or |amax| >= 64, or
-// a non-finite constant. The angle allowance: theta within kDeltaTh, amin / amax rounded to
-// float (U |a| <= kDeltaTh / 2 for |a| < 64) and the subtraction, min and product roundings (3 U
-// |v|): 2 kDeltaTh |1 / norm| + 4 U |v| covers them; e0.w is the first part rounded up.
-enum { RE_WRAP = 1, RE_EXACT = 2 };
-__device__ __forceinline__ void rel_est_consts(const RelConst& rc, float4& e0, float4& e1) {
-    const bool wrap = rc.amin > rc.amax;
-    const double norm = wrap ? rc.norm_w : rc.norm_n;
-    const bool ok = fabs(norm) >= 1e-3 && fabs(rc.amin) < 64.0 && fabs(rc.amax) < 64.0 &&
-                    fabs(rc.start) < 1e30 && fabs(rc.end) < 1e30 && rc.start != 0.0;
-    const float inv_st = ok ? (float)(1.0 / rc.start) : 0.0f;
-    const float ea = ok ? (float)(2.0 * (double)kDeltaTh / fabs(norm) * (1.0 + 0x1p-20)) : 0.0f;
-    e0 = make_float4((float)rc.start, (float)rc.end, inv_st, ea);
-    e1 = make_float4((float)rc.amin, (float)rc.amax, ok ? (float)(1.0 / norm) : 0.0f,
-                     __int_as_float((wrap ? RE_WRAP : 0) | (ok ? 0 : RE_EXACT)));
+// (rel_est_consts: mh_device.h, shared with the host)
+
+// The fp32 PairWise estimate of a relationship from its objects' pose words (the reference's float
+// differences; the distance within 3 U of the reference's double), setting `amb` near the range's
+// ends. e0 = {(float)start, (float)end, 1 / start, -} (rel_est_consts); within kPwEstU U relative.
+__device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& amb) {
+    constexpr float U = 0x1p-24f;
+    const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;
+    const float d2 = fx * fx + fy * fy;
+    const float d = __builtin_amdgcn_sqrtf(d2);  // (1 ulp)
+    const float st = e0.x, en = e0.y;
+    amb |= !(d2 >= 0x1p-100f) || fabsf(d - st) <= 8.0f * U * fabsf(st) ||
+           fabsf(d - en) <= 8.0f * U * fabsf(en);
+    const float f = d < st ? d * e0.z : (d > en ? en * __builtin_amdgcn_rcpf(d) : 0.0f);
+    return (double)(f * f);
 }
+
+// The fp32 PairWiseAngle estimate from theta's estimate `tp` (atan2_est) and the target's pose
+// words, with its absolute allowance `eang`; `amb` near theta's wraps and the wrapped range's
+// switch, for a target rotation outside |rotY| < 16, or where the relationship takes no estimate.
+// e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts).
+__device__ __forceinline__ double rel_ang_est(float4 e1, float ea, ObjP atp, float tp, float& eang,
+                                              bool& amb) {
+    constexpr float U = 0x1p-24f, Y = (float)kTwoPI;
+    const int fl = __float_as_int(e1.w);
+    amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || fabsf(tp) <= kDeltaTh;
+    if (tp < 0.0f) tp = tp + Y;
+    const float t = tp - atp.rotYf;
+    amb |= fabsf(t) <= kDeltaTh;
+    const float th = t < 0.0f ? t + Y : t;
+    bool on;
+    if (fl & RE_WRAP) {
+        // fmodf(x, 2pi) for x in [0, 4pi) is x or x - 2pi, exact (Sterbenz); outside: exact terms
+        const float x = e1.x + th;
+        amb |= !(x >= 0.0f && x < 2.0f * Y);
+        const float w = x >= Y ? x - Y : x;
+        amb |= fabsf(w - e1.y) <= 2.0f * kDeltaTh || fabsf(w) <= 2.0f * kDeltaTh ||
+               fabsf(w - Y) <= 2.0f * kDeltaTh;
+        on = w > e1.y;
+    } else {
+        on = e1.x < th || th < e1.y;  // (continuous at its switch)
+    }
+    const float v = on ? fminf(fabsf(th - e1.x), fabsf(th - e1.y)) * e1.z : 0.0f;
+    eang = ea + 4.0f * U * fabsf(v);
+    return (double)v;
+}
+
+// the focal term's estimate from the focal angle's estimate `at` (Kernel.cu:271, 277)
+__device__ __forceinline__ float cph_est(float at, ObjP p, bool& ambo) {
+    const float ph = (at - p.rotYf) + (float)kHalfPI;
+    ambo |= !(fabsf(p.rotYf) < 16.0f) || !(fabsf(ph) < 16.0f);
+    return cos_est(ph);
+}
+
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q.
 // Split form for callers that batch the atan2: rel_pair() gives the PairWise term and theta's

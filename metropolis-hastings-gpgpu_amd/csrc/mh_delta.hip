@@ -112,6 +112,8 @@ struct DeltaPtrs {
     const RectShape* clrs;  // clearance rectangles, the source object in .pad
     const uint2* rel;       // LDS: relationship objects {s | t << 16, as | at << 16} (hit test)
     const RelConst* relg;   // HBM: the relationship records (read for the ones a move touches)
+    const float4* rele;     // HBM: their fp32 estimate constants, e0[nre] then e1[nre]
+    int nre;                // max(R, 1)
     const DevRoom* rm;
     const float *AREA, *ONES;  // replay streams shared by the workgroup
     const double* ZERO;   // double[DL] zeros
@@ -446,12 +448,22 @@ struct RelBk {
     bool all;
 };
 
+// Terms the plain step holds as fp32 estimates (mh_common.h rel_pw_est, rel_ang_est, cph_est;
+// the full kernel's scheme, §4 of DESIGN.md): this lane's objects t * L + r (bit t of `obj`) and
+// its relationships in slots u < 2 (bit u of `rel`, q = u * L + r), with the angle estimates'
+// allowances. The rejection bound adds their allowances; fix_estimates() makes every one exact
+// before a replay. An undo swaps the record back with the terms (a second undo re-applies it).
+struct EstState {
+    unsigned obj, rel;
+    float eang[2];
+};
+
 // PairWise / PairWiseAngle terms of the relationships touching ka or kb (or all, ka = -2).
 // The hit test reads the relationship objects from LDS; the records themselves (ranges,
 // normalisers) come from HBM, for the few relationships a move touches. `bk`: the overwritten
 // terms are kept there (the proposal's update).
 __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, int kb, int r,
-                                           RelBk* bk = nullptr) {
+                                           RelBk* bk = nullptr, EstState* est = nullptr) {
     uint64_t pend = 0;
     int t = 0;
     for (int q = r; q < nr; q += L, ++t) {
@@ -486,7 +498,24 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
                 bk->cnt = k + 1;
             }
             double tpw, tang;
-            rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
+            bool amb = true;  // (no estimate: the exact terms)
+            if (est && u < 2) {  // the plain step: fp32 estimates with allowances
+                const uint2 w = ch.rel[q];
+                const ObjP ps = obj_pose(ch, (int)(w.x & 0xffffu)), pt = obj_pose(ch, (int)(w.x >> 16));
+                const ObjP as = obj_pose(ch, (int)(w.y & 0xffffu)), atp = obj_pose(ch, (int)(w.y >> 16));
+                const float4 e0 = ch.rele[q], e1 = ch.rele[ch.nre + q];
+                amb = false;
+                tpw = rel_pw_est(e0, ps, pt, amb);
+                const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
+                amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
+                float ea = 0.0f;
+                tang = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
+                const unsigned bit = 1u << u;
+                est->rel = amb ? (est->rel & ~bit) : (est->rel | bit);
+                if (u == 0) est->eang[0] = ea;
+                else est->eang[1] = ea;
+            }
+            if (amb) rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
             ch.RPW[q] = -tpw;
             ch.RANG[q] = -tang;
         }
@@ -639,7 +668,7 @@ __device__ __forceinline__ int build_sa_list(const DeltaPtrs& ch, int n, int c, 
 // build_sa_list), which write the lists as they go.
 template <int S>
 __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, const Own<S>& o, int n, int c,
-                                        int nr, int r) {
+                                        int nr, int r, const EstState& est) {
     BoundTerms bt;
     bt.nx = bt.ny = bt.anx = bt.any = bt.fp = bt.afp = bt.sym = bt.cl = bt.sa = 0.0f;
     bt.symw = bt.clpos = 0.0f;
@@ -671,6 +700,11 @@ __device__ __forceinline__ BoundTerms delta_bound_terms(const DeltaPtrs& ch, con
         bt.aang += fabsf((float)ta);
     }
     bt.k = max(max((n + L - 1) / L, (nr + L - 1) / L), 4 * ((c + n + L - 1) / L));  // uniform
+    // the estimated terms' allowances (EstState): FocalPoint kDeltaCph each, PairWise kPwEstU U
+    // relative (uniform), PairWiseAngle eang each
+    bt.efp = kDeltaCph * (float)__builtin_popcount(est.obj);
+    bt.eang = ((est.rel & 1u) ? est.eang[0] : 0.0f) + ((est.rel & 2u) ? est.eang[1] : 0.0f);
+    bt.pwx = __ballot(est.rel != 0u) ? kPwEstU : 0;
     return bt;
 }
 
@@ -996,13 +1030,55 @@ __device__ __forceinline__ void replay_config(const DeltaPtrs& ch, const typenam
     replay<S>(ch, o, n, cnt_cl, cnt_sa, r, out, dense);
 }
 
+// Makes every estimated term of this lane exact (EstState): the objects' FocalPoint terms and
+// the slots' relationship terms, evaluated as the reference does; check builds verify each
+// estimate against its allowance first (sites 30-32, as in the full kernel).
+template <int S>
+__device__ __forceinline__ void fix_estimates(const DeltaPtrs& ch, const Own<S>& o, EstState& est,
+                                              int r) {
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+        const bool b = ((est.obj >> t) & 1u) != 0;
+        if (__ballot(b) && b) {
+            const int i = t * L + r;
+            const float w = focal_cos(*ch.rm, o.xf[t], o.yf[t], (float)o.ry[t]);
+            MH_CK(fabsf(-ch.CPH[i] - w) <= kDeltaCph, 30, __float_as_uint(-ch.CPH[i]),
+                  __float_as_uint(w));
+            ch.CPH[i] = -w;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bool b = ((est.rel >> u) & 1u) != 0;
+        if (__ballot(b) && b) {
+            const int q = u * L + r;
+            double tpw, tang;
+            rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
+            MH_CK(fabs(-ch.RPW[q] - tpw) <= kPwEstU * 0x1p-24 * fabs(tpw) + 1e-30, 31,
+                  __float_as_uint((float)-ch.RPW[q]), __float_as_uint((float)tpw));
+            MH_CK(fabs(-ch.RANG[q] - tang) <= (double)est.eang[u], 32,
+                  __float_as_uint((float)-ch.RANG[q]), __float_as_uint((float)tang));
+            ch.RPW[q] = -tpw;
+            ch.RANG[q] = -tang;
+        }
+    }
+    est.obj = est.rel = 0u;
+    wave_sync();
+}
+
 // Undoes the last proposal (objects ka, kb): the backed-up poses and FocalPoint terms, the
 // SurfaceArea bits (SAM <-> SAMB, so the proposal's bits stay in SAMB), the clearance boxes and
 // pair bits, the relationship terms.
 template <int S>
 __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, int n, int c, int nr,
                                               int ka, int kb, int r, bool writer, RelBk& rbk,
-                                              typename Own<S>::wvec& bk_nz) {
+                                              typename Own<S>::wvec& bk_nz, EstState& est,
+                                              EstState& est_bk) {
+    {  // the estimate record of the terms restored below (a swap, as the terms)
+        const EstState t = est;
+        est = est_bk;
+        est_bk = t;
+    }
     const int nb = ch.aux->nb;
     for (int q = nb - 1; q >= 0; --q) {
         const DBackup b = ch.aux->b[q];
@@ -1090,6 +1166,8 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     ch.clrs = clrs_l;
     ch.rel = rel_l;
     ch.relg = a.relc;
+    ch.rele = a.rele;
+    ch.nre = nr > 0 ? nr : 1;
     ch.rm = rm_l;
     ch.AREA = reinterpret_cast<const float*>(lds + lay.h_area);
     ch.ONES = reinterpret_cast<const float*>(lds + lay.h_ones);
@@ -1207,6 +1285,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     // costs: the current total is then known as an interval (cur_iv, cur_exact false) until a
     // step's decision needs it exactly, or the launch ends.
     bool cur_exact = true;
+    EstState est{0u, 0u, {0.0f, 0.0f}};  // (the launch starts with exact terms)
     CostIv cur_iv{cur_total, cur_total};
     typename RngOf<XW, L>::type rng;
     rng_load(rng, a, chain, m0);
@@ -1234,11 +1313,23 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         int dwild = 0;
         const double rka = obj_ry<S>(o, ka < 0 ? 0 : ka), rkb = obj_ry<S>(o, kb < 0 ? 0 : kb);
         float sv_obj = 0.0f, sv_clr = 0.0f;  // (lanes 0, 1: the moved objects' SurfaceArea sums)
+        EstState est_bk = est;  // (the undo's record, undo_proposal)
+        bool kest = false;      // (lanes 0, 1: their object's FocalPoint term is an estimate)
         if (r < 2) {
             const int k = r == 0 ? ka : kb;
             if (k >= 0) {
                 const ObjP p = obj_pose(ch, k);
-                ch.CPH[k] = -focal_cos(*rm_l, p.xf, p.yf, p.rotYf);
+                // the plain step's FocalPoint estimate (exact where cph_est cannot vouch for it)
+                bool ambo = true;
+                float w = 0.0f;
+                if constexpr (!TRACK) {
+                    const float fy = rm_l->fyf - p.yf, fx = rm_l->fxf - p.xf;
+                    ambo = !(fmaxf(fabsf(fy), fabsf(fx)) >= 0x1p-100f);
+                    w = cph_est(atan2_est(fy, fx), p, ambo);
+                }
+                if (ambo) w = focal_cos(*rm_l, p.xf, p.yf, p.rotYf);
+                ch.CPH[k] = -w;
+                kest = !ambo;
                 const float4 vo = comp_overlaps(*rm_l, ch.BOX[k]);
                 sam_put(ch, c + k, nonzero4(vo));
                 sv_obj = nonzero4(vo) ? (vo.x + vo.y) + (vo.z + vo.w) : 0.0f;
@@ -1253,13 +1344,21 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             }
         }
         const int wild_star = wild_cnt + __shfl(dwild, 0) + __shfl(dwild, 1);
+        if constexpr (!TRACK) {  // the moved objects' owner lanes record the estimates
+            const bool ea = __builtin_amdgcn_readlane((int)kest, 0) != 0;
+            const bool eb = __builtin_amdgcn_readlane((int)kest, 1) != 0;
+            if (ka >= 0 && r == (ka & 63))
+                est.obj = ea ? (est.obj | (1u << (ka >> 6))) : (est.obj & ~(1u << (ka >> 6)));
+            if (kb >= 0 && r == (kb & 63))
+                est.obj = eb ? (est.obj | (1u << (kb >> 6))) : (est.obj & ~(1u << (kb >> 6)));
+        }
         wave_sync();
         DSTAMP(0);
         typename Own<S>::wvec bk_nz = o.nz0;  // (the undo's record, undo_proposal)
         const bool chg0 = clearance_delta<S>(ch, o, n, c, ka, kb, r);
         DSTAMP(1);
         RelBk rbk;
-        rels_delta(ch, nr, ka, kb, r, &rbk);
+        rels_delta(ch, nr, ka, kb, r, &rbk, TRACK ? nullptr : &est);
         DSTAMP(2);
         symmetry_delta<S>(ch, o, n, ka, kb, wild_star > 0, r);
         wave_sync();
@@ -1331,7 +1430,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 #endif
         if constexpr (FASTD) {
             u_acc = rng.uniform();
-            BoundTerms bt = delta_bound_terms<S>(ch, o, n, c, nr, r);
+            BoundTerms bt = delta_bound_terms<S>(ch, o, n, c, nr, r, est);
             bt.cl = clsum;
             bt.kcl = kcl;
             bt.clpos = clpos;
@@ -1357,6 +1456,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         float chk_star = 0.0f;
         if (FASTD && bd != BOUND_OPEN) {
             float ro[8];
+            fix_estimates<S>(ch, o, est, r);  // (the check's replay needs the exact terms)
             replay_config<S>(ch, o.pmx, o, n, cnt_cl, cnt_sa, r, ro);
             chk_star = uniform_f(ro[0]);
             const bool acc_x = u_acc < accept_threshold(kBeta * ((double)chk_star - (double)chk_cur));
@@ -1378,6 +1478,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         bool rare = false;  // the exact pass of the current configuration ran (below)
         int bd2 = BOUND_OPEN;  // an open step decided by its exact total against the interval
         if (bd == BOUND_OPEN) {
+        if constexpr (!TRACK) fix_estimates<S>(ch, o, est, r);  // (the replay reads exact terms)
         if (!cl_built) build_cl_list<S>(ch, o, c, r, 0);  // (the lists the replay walks)
         if (!sa_built) cnt_sa = build_sa_list(ch, n, c, r, 0);
 #if MH_STAMPS > 1
@@ -1440,11 +1541,12 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             const int nb = ch.aux->nb;
             const DBackup p0 = read_obj<S>(ch, o, nb > 0 ? ch.aux->b[0].k : 0);
             const DBackup p1 = read_obj<S>(ch, o, nb > 1 ? ch.aux->b[1].k : 0);
-            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz);
+            undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz, est, est_bk);
             if (writer) {
                 if (nb > 0) ch.aux->b[0] = p0;
                 if (nb > 1) ch.aux->b[1] = p1;
             }
+            if constexpr (!TRACK) fix_estimates<S>(ch, o, est, r);  // (the current configuration's)
             lcl = build_cl_list<S>(ch, o, c, r, 0);
             lsa = build_sa_list(ch, n, c, r, 0);
             rare = true;
@@ -1470,7 +1572,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         else acc = u_acc < accept_threshold(kBeta * ((double)sc[0] - (double)cur_total));
         // A rejected proposal is undone; after the exact pass of the current configuration
         // (rare) the state is the current one, and an accepted proposal is re-applied.
-        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz);
+        if (acc == rare) undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz, est, est_bk);
         if (acc) {
             ++accepted;
 #if MH_CHECK

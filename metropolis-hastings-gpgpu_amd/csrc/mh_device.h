@@ -56,6 +56,41 @@ struct RelConst {   // relationship i: rss[i] and rsa[i] (sized by nRelationship
     double norm_n;      // (2PI - (amax - amin)) / 2, Kernel.cu:255 (plain range)
 };
 
+// Allowances of the rejection bound's fp32 estimates (derivation: mh_common.h, above atan2_est).
+constexpr float kDeltaCph = 0x1p-17f;
+constexpr float kDeltaTh = 0x1p-17f;
+constexpr int kPwEstU = 20;
+
+// The fp32 constants of relationship i's estimates (two float4 per relationship; the
+// full-evaluation kernel stages them in LDS, the incremental kernel reads them from HBM with the
+// records a move touches -- built on the host, LaunchArgs::rele):
+//   e0 = {(float)start, (float)end, 1 / start, the angle allowance's constant part}
+//   e1 = {(float)amin, (float)amax, 1 / norm of the range (wrapped or plain), flags}
+// flags: bit 0 the range wraps (amin > amax, Kernel.cu:245); bit 1 no estimate (the term is
+// always evaluated exactly): a degenerate normaliser (|norm| < 1e-3), |amin| or |amax| >= 64, or
+// a non-finite constant. The angle allowance: theta within kDeltaTh, amin / amax rounded to
+// float (U |a| <= kDeltaTh / 2 for |a| < 64) and the subtraction, min and product roundings (3 U
+// |v|): 2 kDeltaTh |1 / norm| + 4 U |v| covers them; e0.w is the first part rounded up.
+enum { RE_WRAP = 1, RE_EXACT = 2 };
+template <class F4>
+inline MH_HD void rel_est_consts(const RelConst& rc, F4& e0, F4& e1) {
+    const bool wrap = rc.amin > rc.amax;
+    const double norm = wrap ? rc.norm_w : rc.norm_n;
+    const double an = norm < 0 ? -norm : norm;
+    const double a0 = rc.amin < 0 ? -rc.amin : rc.amin, a1 = rc.amax < 0 ? -rc.amax : rc.amax;
+    const double s0 = rc.start < 0 ? -rc.start : rc.start, s1 = rc.end < 0 ? -rc.end : rc.end;
+    const bool ok = an >= 1e-3 && a0 < 64.0 && a1 < 64.0 && s0 < 1e30 && s1 < 1e30 &&
+                    rc.start != 0.0;
+    e0.x = (float)rc.start;
+    e0.y = (float)rc.end;
+    e0.z = ok ? (float)(1.0 / rc.start) : 0.0f;
+    e0.w = ok ? (float)(2.0 * (double)kDeltaTh / an * (1.0 + 0x1p-20)) : 0.0f;
+    e1.x = (float)rc.amin;
+    e1.y = (float)rc.amax;
+    e1.z = ok ? (float)(1.0 / norm) : 0.0f;
+    e1.w = __builtin_bit_cast(float, (wrap ? RE_WRAP : 0) | (ok ? 0 : RE_EXACT));
+}
+
 // Scalars of one room, passed by value as a kernel argument.
 struct DevRoom {
     int n, c, r, pad0;

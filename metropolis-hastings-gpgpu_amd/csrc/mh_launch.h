@@ -25,6 +25,7 @@ struct LaunchArgs {
     const ObjConst* objc;
     const ClrConst* clrc;
     const RelConst* relc;
+    const float4* rele;      // [2][R] the relationships' fp32 estimate constants (rel_est_consts)
     const double* cfg;       // OP_INIT: [6][N] initial pose; OP_EVAL: [n_chains][6][N]
     double* st;              // [n_chains][6][N] chain poses
     ChainMeta* meta;         // [n_chains]

@@ -23,6 +23,9 @@ SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept
          27: "cached Clearance row sums differ from a fresh build",
          28: "cached Clearance column sum differs from a fresh one",
          29: "cached SurfaceArea sums differ from a fresh build",
+         30: "a FocalPoint estimate outside kDeltaCph",
+         31: "a PairWise estimate outside kPwEstU U",
+         32: "a PairWiseAngle estimate outside its allowance",
          33: "a deferred Symmetry row maximum outside its estimate's allowance"}
 
 # (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
