@@ -1049,6 +1049,9 @@ template <bool DPW = false>
 __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
                                             const BoundTerms& bt, float u, CostIv cur,
                                             CostIv& star, float slack = 1.0f) {
+    // (fused multiply-adds allowed here: every rounding below is counted in the allowance, and
+    // a fused operation rounds once where the count assumes two)
+#pragma clang fp contract(fast)
     constexpr float U = 0x1p-24f;
     const float kf = (float)bt.k;
     const float lfp = rm.w_fp * bt.fp, lsym = rm.w_sym * bt.sym, lcl = rm.w_cl * bt.cl,
