@@ -711,6 +711,7 @@ __device__ __forceinline__ float sym_val_fast(float4 q, float rx, float ry, floa
 // (12.6 + 2|v| + |rr|) x 0.4, the fp32 combine <= 2^-23 (15 + 2|v|) and the reference's own
 // final rounding 2^-24 |v|; together < 2^-21 (12 + 2.2|v| + 0.1|rr|). A 4x margin gives:
 __device__ __forceinline__ float sym_err(float v, float rr) {
+#pragma clang fp contract(fast)  // (an allowance with a 4x margin: one rounding fewer is immaterial)
     return 0x1p-19f * (12.0f + 3.0f * fabsf(v) + fabsf(rr));
 }
 
@@ -1262,6 +1263,7 @@ __device__ __forceinline__ float cos_est(float x) {
 // differences; the distance within 3 U of the reference's double), setting `amb` near the range's
 // ends. e0 = {(float)start, (float)end, 1 / start, -} (rel_est_consts); within kPwEstU U relative.
 __device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& amb) {
+#pragma clang fp contract(fast)  // (fused: fewer roundings than the allowance counts)
     constexpr float U = 0x1p-24f;
     const float fx = ps.xf - pt.xf, fy = ps.yf - pt.yf;
     const float d2 = fx * fx + fy * fy;
@@ -1279,6 +1281,7 @@ __device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& 
 // e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts).
 __device__ __forceinline__ double rel_ang_est(float4 e1, float ea, ObjP atp, float tp, float& eang,
                                               bool& amb) {
+#pragma clang fp contract(fast)  // (fused: fewer roundings than the allowance counts)
     constexpr float U = 0x1p-24f, Y = (float)kTwoPI;
     const int fl = __float_as_int(e1.w);
     amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || fabsf(tp) <= kDeltaTh;
