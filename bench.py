@@ -199,6 +199,10 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-iters", type=int, default=4000,
                     help="MH steps of the end-to-end KernelWrapperSeeded leg (0: skip)")
+    ap.add_argument("--collective", action="store_true",
+                    help="run the process group and the best-cost all-gather even at world size "
+                         "1 (the RCCL leg on device tensors with one GPU; launched without "
+                         "torch.distributed.run it rendezvouses on 127.0.0.1)")
     args = ap.parse_args()
     args.iters = max(1, args.iters)
     launches_per_step = -(-args.iters // STEPS_PER_LAUNCH)
@@ -220,7 +224,16 @@ def main() -> int:
                          f"multi-rank path on fewer GPUs)")
     device = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
-    if world > 1:
+    # The collective leg runs whenever there is more than one rank, or on request at one rank.
+    use_dist = world > 1 or args.collective
+    if use_dist and "MASTER_ADDR" not in os.environ:  # (a plain `python bench.py --collective`)
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                          WORLD_SIZE="1")
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -245,7 +258,7 @@ def main() -> int:
     for _ in range(args.warmup):
         sess.run(args.iters, handle)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -256,7 +269,7 @@ def main() -> int:
         sess.run(args.iters, handle)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -276,7 +289,7 @@ def main() -> int:
     me = torch.tensor([rank, device, *pci, wall, kernel_ms, offset, count], dtype=torch.float64,
                       device=cdev)
     ranks = None
-    if world > 1:
+    if use_dist:
         gathered = [torch.empty_like(rec) for _ in range(world)]
         dist.all_gather(gathered, rec)
         everyone = [torch.empty_like(me) for _ in range(world)]
@@ -384,13 +397,13 @@ def main() -> int:
                 "distinct_gpus": len({(d["pci_domain"], d["pci_bus"], d["pci_device"])
                                       for d in ranks}),
                 "ranks": ranks,
-            } if world > 1 else None),
+            } if use_dist else None),
             "e2e_chain_steps_per_s": e2e["chain_steps_per_s"] if e2e else None,
             "e2e": e2e,
         }
         print(json.dumps(out), flush=True)
     sess.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     return 0
 

@@ -196,6 +196,12 @@ MH_API result* KernelWrapperEx(relationshipStruct* rss, relationshipAngleStruct*
 /* Frees a KernelWrapper result (the points block and the array). NULL is a no-op. */
 MH_API void KernelFreeResult(result* res);
 
+/* Frees the device memory, streams and pinned staging that KernelWrapper keeps between calls
+ * (at most two idle sessions per device; $MH_WRAPPER_CACHE=0 keeps none). Returns the number of
+ * sessions freed. Calls in flight are unaffected. (No reference counterpart: the reference
+ * allocates and leaks per call, Kernel.cu:926-967.) */
+MH_API int KernelReleaseCache(void);
+
 /* Text of the last error on the calling thread ("" if none). */
 MH_API const char* KernelLastError(void);
 
@@ -284,6 +290,13 @@ MH_API void mh_session_destroy(mh_session* s);
  * over groups of L = 8, 16, 32 or 64 lanes), run on the current device for the 64 lane values
  * v (floats) and iv (ints); out receives 9 x 64 ints (layout in mh_chain.hip). Returns 0. */
 MH_API int mh_debug_collectives(int L, const float* v, const int* iv, int* out);
+
+/* The step kernel the calling thread's last KernelWrapper* call ran (its first shard): lanes per
+ * chain and kind, coded as mh_session_geometry codes them. Returns -1 before any call. (The
+ * pooled sessions keep their kernel choice only while the room shape, chain count, options and
+ * the tuning overrides $MH_LANES / $MH_WAVES / $MH_STEP_FEW / $MH_SPEC / $MH_DELTA /
+ * $MH_DELTA_WAVES are unchanged; this lets a test see that.) */
+MH_API int mh_debug_wrapper_step(int* lanes_per_chain, int* kind);
 
 MH_API int mh_debug_rng(uint64_t seed, uint64_t subsequence, int n, unsigned int* out_u32,
                         float* out_uniform, float* out_normal);

@@ -121,12 +121,12 @@ COST_FIELDS = ["totalCosts", "PairWiseCosts", "VisualBalanceCosts", "FocalPointC
 
 # Every symbol include/mh_kernel.h declares.
 EXPORTS = ["KernelWrapper", "KernelWrapperSeeded", "KernelWrapperEx", "KernelFreeResult",
-           "KernelLastError", "KernelEvaluateCosts", "mh_session_create", "mh_session_create_ex",
+           "KernelReleaseCache", "KernelLastError", "KernelEvaluateCosts", "mh_session_create", "mh_session_create_ex",
            "mh_session_run", "mh_session_finalize",
            "mh_session_download", "mh_session_current_costs", "mh_session_summary",
            "mh_session_geometry", "mh_session_occupancy",
            "mh_session_destroy", "mh_debug_rng", "mh_debug_rng_ex", "mh_debug_collectives",
-           "mh_debug_math"]
+           "mh_debug_math", "mh_debug_wrapper_step"]
 
 P = C.POINTER
 
@@ -177,6 +177,9 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.KernelWrapperEx.restype = P(result)
     lib.KernelFreeResult.argtypes = [P(result)]
     lib.KernelFreeResult.restype = None
+    if hasattr(lib, "KernelReleaseCache"):  # (A/B variants of earlier revisions lack it)
+        lib.KernelReleaseCache.argtypes = []
+        lib.KernelReleaseCache.restype = C.c_int
     lib.KernelLastError.argtypes = []
     lib.KernelLastError.restype = C.c_char_p
     lib.KernelEvaluateCosts.argtypes = [P(relationshipStruct), P(relationshipAngleStruct),
@@ -204,6 +207,9 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.mh_session_occupancy.restype = C.c_int
     lib.mh_session_destroy.argtypes = [C.c_void_p]
     lib.mh_session_destroy.restype = None
+    if hasattr(lib, "mh_debug_wrapper_step"):  # (A/B variants of earlier revisions lack it)
+        lib.mh_debug_wrapper_step.argtypes = [P(C.c_int), P(C.c_int)]
+        lib.mh_debug_wrapper_step.restype = C.c_int
     lib.mh_debug_collectives.argtypes = [C.c_int, P(C.c_float), P(C.c_int), P(C.c_int)]
     lib.mh_debug_collectives.restype = C.c_int
     lib.mh_debug_rng.argtypes = [C.c_uint64, C.c_uint64, C.c_int, P(C.c_uint32), P(C.c_float),
@@ -303,6 +309,23 @@ def kernel_wrapper(room: Room, chains: int, iterations: int, seed: int | None = 
     finally:
         lib.KernelFreeResult(res)
     return p, costs
+
+
+STEP_KINDS = {0: "full", 1: "incremental", 2: "full-few", 3: "speculative"}
+
+
+def wrapper_step_kernel():
+    """(lanes per chain, kind) of the step kernel this thread's last kernel_wrapper call ran."""
+    lib = load_library()
+    lanes, kind = C.c_int(), C.c_int()
+    if lib.mh_debug_wrapper_step(C.byref(lanes), C.byref(kind)) != 0:
+        raise MHError("no KernelWrapper call on this thread yet")
+    return lanes.value, STEP_KINDS[kind.value]
+
+
+def release_cache() -> int:
+    """KernelReleaseCache(): frees KernelWrapper's idle pooled sessions; returns how many."""
+    return int(load_library().KernelReleaseCache())
 
 
 def evaluate_costs(room: Room, cfgs) -> np.ndarray:
@@ -433,8 +456,7 @@ class Session:
         with as few chains: mh_spec.hip)."""
         lanes, cpw, inc = C.c_int(), C.c_int(), C.c_int()
         self.lib.mh_session_geometry(self.h, C.byref(lanes), C.byref(cpw), C.byref(inc))
-        return lanes.value, cpw.value, {0: "full", 1: "incremental", 2: "full-few",
-                                        3: "speculative"}[inc.value]
+        return lanes.value, cpw.value, STEP_KINDS[inc.value]
 
     def occupancy(self) -> int:
         """Chains of the step kernel one CU keeps resident (the runtime's occupancy count)."""

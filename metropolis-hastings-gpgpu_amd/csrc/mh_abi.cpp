@@ -34,6 +34,9 @@ static_assert((int)mh::TRACK_OFF == MH_TRACK_OFF && (int)mh::TRACK_LOWEST == MH_
 namespace {
 
 thread_local std::string g_last_error;
+// The step kernel of this thread's last KernelWrapper call (mh_debug_wrapper_step): lanes per
+// chain and kind as mh_session_geometry reports them; -1 before any call.
+thread_local int g_wrapper_lanes = -1, g_wrapper_kind = -1;
 
 void set_error(const std::string& e) { g_last_error = e; }
 
@@ -402,6 +405,12 @@ struct mh_session {
     point* d_pts = nullptr;
     resultCosts* d_costs = nullptr;
     mh_summary* d_summary = nullptr;
+    // Download staging: two pinned chunks the library allocates (hipHostMalloc) and owns. A
+    // download DMAs chunk k into one while the host copies chunk k - 1 out of the other into the
+    // caller's buffer, which is never page-locked (hipHostRegister) -- see copy_out.
+    unsigned char* h_stage = nullptr;
+    size_t stage_chunk = 0;
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
     // Element capacities of the buffers above: a pooled session (KernelWrapper's cache) keeps
     // its buffers across calls and grows one only when a call needs more.
     size_t cap_obj = 0, cap_clr = 0, cap_rel = 0, cap_rele = 0, cap_cfg0 = 0, cap_st = 0, cap_best = 0,
@@ -412,6 +421,7 @@ struct mh_session {
     int geo_n = -1, geo_c = -1, geo_r = -1;
     int64_t geo_chains = -1;
     bool geo_plain = false;
+    std::string geo_env;  // the tuning overrides choose_geometry read (geometry_env)
 
     static float bound_slack() {
         const char* e = getenv("MH_BOUND_SLACK");
@@ -471,6 +481,9 @@ void free_session(mh_session* s) {
     (void)hipFree(s->d_pts);
     (void)hipFree(s->d_costs);
     (void)hipFree(s->d_summary);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
+    for (hipEvent_t e : s->stage_ev)
+        if (e) (void)hipEventDestroy(e);
     if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     (void)hipSetDevice(prev);
@@ -515,6 +528,21 @@ bool record_done(mh_session* s, hipStream_t st) {
     return true;
 }
 
+// The environment overrides choose_geometry (and choose_lanes, choose_delta_geometry) reads. A
+// pooled session keeps its geometry only while these are unchanged too, so a KernelWrapper call
+// made after one of them changed runs the kernel it names, not the previous call's.
+std::string geometry_env() {
+    static const char* const kVars[] = {"MH_LANES", "MH_WAVES", "MH_STEP_FEW", "MH_SPEC",
+                                        "MH_DELTA", "MH_DELTA_WAVES"};
+    std::string key;
+    for (const char* v : kVars) {
+        const char* e = getenv(v);
+        key += e ? e : "-";
+        key += '\x1f';
+    }
+    return key;
+}
+
 // Sets a session up for its room, chains and options. A pooled session (KernelWrapper's cache)
 // comes here again for every call: its stream and event are kept, its buffers grow only when
 // too small, and the geometry is chosen again only for another room shape or chain count.
@@ -526,8 +554,9 @@ bool session_init(mh_session* s) {
     s->steps_done = 0;
     const bool plain = s->track == mh::TRACK_OFF && s->n_temps <= 1 && s->rng == mh::RNG_PHILOX;
     const int rn = s->room.rm.n, rc = s->room.rm.c, rr = s->room.rm.r;
+    const std::string env = geometry_env();
     if (!(s->geo_valid && s->geo_n == rn && s->geo_c == rc && s->geo_r == rr &&
-          s->geo_chains == s->n_chains && s->geo_plain == plain)) {
+          s->geo_chains == s->n_chains && s->geo_plain == plain && s->geo_env == env)) {
         s->geo_valid = false;
         if (!choose_geometry(rn, rc, rr, s->device, s->n_chains, plain, s->geo)) return false;
         s->geo_valid = true;
@@ -536,6 +565,7 @@ bool session_init(mh_session* s) {
         s->geo_r = rr;
         s->geo_chains = s->n_chains;
         s->geo_plain = plain;
+        s->geo_env = env;
     }
     if (!upload(&s->d_obj, s->cap_obj, s->room.obj, s->stream)) return false;
     if (!upload(&s->d_clr, s->cap_clr, s->room.clr, s->stream)) return false;
@@ -601,22 +631,33 @@ bool session_finalize(mh_session* s, hipStream_t st) {
     return record_done(s, st);
 }
 
-// Downloads below this size never page-lock the caller's buffer.
-constexpr size_t kLockMinBytes = 1u << 20;
+// Bytes per download staging chunk (two are held per session: 8 MB of pinned host memory).
+constexpr size_t kStageChunk = 4u << 20;
 
-// $MH_DOWNLOAD_PAGEABLE=1: downloads never page-lock the caller's buffer (the staged copy only,
-// for the A/B of the two).
-bool download_pageable() {
-    static const bool pageable = getenv("MH_DOWNLOAD_PAGEABLE") && atoi(getenv("MH_DOWNLOAD_PAGEABLE"));
-    return pageable;
+// The session's pinned staging chunks, at least min(bytes, kStageChunk) each.
+bool ensure_stage(mh_session* s, size_t bytes) {
+    const size_t want = std::min(bytes, kStageChunk);
+    if (!s->stage_ev[0]) MH_TRY_HIP(hipEventCreateWithFlags(&s->stage_ev[0], hipEventDisableTiming));
+    if (!s->stage_ev[1]) MH_TRY_HIP(hipEventCreateWithFlags(&s->stage_ev[1], hipEventDisableTiming));
+    if (s->h_stage && s->stage_chunk >= want) return true;
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
+    s->h_stage = nullptr;
+    s->stage_chunk = 0;
+    const size_t chunk = (want + 4095) & ~(size_t)4095;
+    MH_TRY_HIP(hipHostMalloc((void**)&s->h_stage, 2 * chunk, hipHostMallocDefault));
+    s->stage_chunk = chunk;
+    return true;
 }
 
-// Copies `bytes` from device memory into a caller's host buffer on the session's stream, ordered
-// after the session's work. Unless `locked_by_caller` (KernelWrapper page-locks its whole result
-// once, before its per-device threads start: shards of one buffer share boundary pages, which
-// two threads must not lock and unlock independently), the host range is page-locked for the
-// copy so the DMA runs straight into it; where it cannot be locked, a plain staged copy.
-bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes, bool locked_by_caller) {
+// Copies `bytes` from device memory into a caller's host buffer, ordered after the session's
+// work (the reference's plain D2H copies, Kernel.cu:959-960). The caller's memory is only ever
+// written by the host: the DMA lands in the session's own pinned chunks and the host copies each
+// chunk out while the next one is in flight. (Round 5 page-locked the caller's buffer instead --
+// hipHostRegister on whatever heap pages it shared with the caller's other objects -- and saw two
+// "illegal memory access" reports at this point; DESIGN.md section 7 "The round-5 download
+// fault".) Thread-safe across sessions: each shard of a KernelWrapper call writes a disjoint
+// slice through its own session's chunks.
+bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes) {
     if (bytes == 0) return true;
     hipStream_t st = s->stream;
     if (!order_after_last(s, st)) return false;
@@ -626,37 +667,38 @@ bool copy_out(mh_session* s, void* host, const void* dev, size_t bytes, bool loc
                   hipGetErrorString(ek));
         return false;
     }
-    // Small results take the runtime's staged copy: page-locking a few unaligned pages of the
-    // caller's heap per call buys nothing there.
-    const bool locked = !locked_by_caller && !download_pageable() && bytes >= kLockMinBytes &&
-                        hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
-    if (!locked) (void)hipGetLastError();  // (clear the sticky error of the failed lock)
-    MH_TRY_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
-    const hipError_t e = hipStreamSynchronize(st);
-    if (locked) (void)hipHostUnregister(host);
-    MH_TRY_HIP(e);
+    if (!ensure_stage(s, bytes)) return false;
+    const size_t chunk = s->stage_chunk;
+    const size_t chunks = (bytes + chunk - 1) / chunk;
+    auto len = [&](size_t k) { return std::min(chunk, bytes - k * chunk); };
+    // Chunk k goes to staging half k & 1; that half's previous chunk (k - 2) was copied out by
+    // the host in iteration k - 1, so it is free.
+    for (size_t k = 0; k <= chunks; ++k) {
+        if (k < chunks) {
+            MH_TRY_HIP(hipMemcpyAsync(s->h_stage + (k & 1) * chunk,
+                                      static_cast<const unsigned char*>(dev) + k * chunk, len(k),
+                                      hipMemcpyDeviceToHost, st));
+            MH_TRY_HIP(hipEventRecord(s->stage_ev[k & 1], st));
+        }
+        if (k > 0) {
+            const size_t j = k - 1;
+            MH_TRY_HIP(hipEventSynchronize(s->stage_ev[j & 1]));
+            memcpy(static_cast<unsigned char*>(host) + j * chunk, s->h_stage + (j & 1) * chunk,
+                   len(j));
+        }
+    }
     return record_done(s, st);
 }
 
 // The session's final points and costs, after all of its queued work (an event wait, so another
 // session's work on the same device is not waited for).
-bool session_download(mh_session* s, point* pts, resultCosts* costs, bool locked_by_caller = false) {
+bool session_download(mh_session* s, point* pts, resultCosts* costs) {
     MH_TRY_HIP(hipSetDevice(s->device));
     const size_t n = (size_t)s->room.rm.n;
     if (s->n_chains <= 0) return true;
-    if (pts && !copy_out(s, pts, s->d_pts, sizeof(point) * n * s->n_chains, locked_by_caller))
-        return false;
-    if (costs && !copy_out(s, costs, s->d_costs, sizeof(resultCosts) * s->n_chains, locked_by_caller))
-        return false;
+    if (pts && !copy_out(s, pts, s->d_pts, sizeof(point) * n * s->n_chains)) return false;
+    if (costs && !copy_out(s, costs, s->d_costs, sizeof(resultCosts) * s->n_chains)) return false;
     return true;
-}
-
-// Page-locks a host range for every device (portable), or leaves it pageable (false).
-bool lock_host(void* p, size_t bytes) {
-    if (bytes == 0 || download_pageable()) return false;
-    if (hipHostRegister(p, bytes, hipHostRegisterPortable) == hipSuccess) return true;
-    (void)hipGetLastError();  // (clear the sticky error of the failed lock)
-    return false;
 }
 
 // ---- KernelWrapper's session cache -----------------------------------------------------------
@@ -668,8 +710,10 @@ bool lock_host(void* p, size_t bytes) {
 // (a buffer grows only when a call needs more) and the geometry is kept while the room's shape
 // and the chain count stay the same. Thread-safe: a mutex per device, and concurrent calls
 // borrow different sessions (at most kPoolKeep idle ones are kept per device). The pool is never
-// destroyed: freeing device memory from a static destructor would run after the HIP runtime's
-// own teardown; the process's exit releases it. $MH_WRAPPER_CACHE=0 turns the cache off.
+// destroyed implicitly: freeing device memory from a static destructor would run after the HIP
+// runtime's own teardown, so the process's exit releases it, and a host application that shares
+// the GPU calls KernelReleaseCache() to free the idle sessions earlier (a config-3-shaped call
+// leaves ~0.3 GB per session on the device). $MH_WRAPPER_CACHE=0 turns the cache off.
 constexpr int kPoolDevices = 64;
 constexpr size_t kPoolKeep = 2;
 
@@ -683,9 +727,29 @@ SessionPool* session_pools() {
     return pools;
 }
 
+// (read on every call: turning the cache off later in a process takes effect at the next call)
 bool wrapper_cache_on() {
-    static const bool on = !(getenv("MH_WRAPPER_CACHE") && atoi(getenv("MH_WRAPPER_CACHE")) == 0);
-    return on;
+    const char* e = getenv("MH_WRAPPER_CACHE");
+    return !(e && *e && atoi(e) == 0);
+}
+
+// Frees every idle pooled session (their device buffers, streams and pinned staging); returns
+// how many. Sessions borrowed by calls in flight go back to the pool as usual afterwards.
+int release_pools() {
+    int freed = 0;
+    for (int d = 0; d < kPoolDevices; ++d) {
+        SessionPool& p = session_pools()[d];
+        std::vector<mh_session*> idle;
+        {
+            std::lock_guard<std::mutex> lk(p.mu);
+            idle.swap(p.idle);
+        }
+        for (mh_session* s : idle) {
+            free_session(s);
+            ++freed;
+        }
+    }
+    return freed;
 }
 
 bool configure_session(mh_session* s, const Room& room, int device, int64_t n_chains,
@@ -822,6 +886,7 @@ bool devices_from_env(int current, std::vector<int>& d) {
 struct Shard {
     int device;
     int64_t begin, count;
+    int lanes = -1, kind = -1;  // the step kernel its session ran (mh_session_geometry's codes)
     bool ok = false;
     std::string err;
 };
@@ -873,18 +938,15 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
         shards[k].begin = K * (groups * (int64_t)k / (int64_t)devs.size());
         shards[k].count = K * (groups * (int64_t)(k + 1) / (int64_t)devs.size()) - shards[k].begin;
     }
-    // The result buffers are page-locked once, here, for all shards (a shard's slice shares its
-    // boundary pages with its neighbours'); if they cannot be, every shard copies staged.
-    const bool locked_pts = lock_host(pts, sizeof(point) * n * (size_t)chains);
-    const bool locked_costs = lock_host(costs.data(), sizeof(resultCosts) * (size_t)chains);
     auto work = [&](Shard& sh) {
         mh_session* s = session_borrow(room, sh.device, sh.count, sh.begin, opts);
         if (!s) {
             sh.err = g_last_error;
             return;
         }
+        (void)mh_session_geometry(s, &sh.lanes, nullptr, &sh.kind);
         sh.ok = session_run(s, iterations, s->stream) && session_finalize(s, s->stream) &&
-                session_download(s, pts + n * sh.begin, costs.data() + sh.begin, true);
+                session_download(s, pts + n * sh.begin, costs.data() + sh.begin);
         if (!sh.ok) {
             sh.err = g_last_error;
             free_session(s);  // (a failed session is not reused)
@@ -894,14 +956,16 @@ result* wrapper_impl(relationshipStruct* rss, relationshipAngleStruct* rsa, posi
     };
     if (shards.size() == 1) {
         work(shards[0]);
+        g_wrapper_lanes = shards[0].lanes;
+        g_wrapper_kind = shards[0].kind;
     } else {
         std::vector<std::thread> th;
         for (auto& sh : shards) th.emplace_back(work, std::ref(sh));
         for (auto& t : th) t.join();
+        g_wrapper_lanes = shards[0].lanes;
+        g_wrapper_kind = shards[0].kind;
     }
     (void)hipSetDevice(current);
-    if (locked_pts) (void)hipHostUnregister(pts);
-    if (locked_costs) (void)hipHostUnregister(costs.data());
     for (auto& sh : shards) {
         if (!sh.ok) {
             free(pts);
@@ -957,6 +1021,20 @@ MH_API void KernelFreeResult(result* res) {
 }
 
 MH_API const char* KernelLastError(void) { return g_last_error.c_str(); }
+
+MH_API int mh_debug_wrapper_step(int* lanes_per_chain, int* kind) {
+    if (lanes_per_chain) *lanes_per_chain = g_wrapper_lanes;
+    if (kind) *kind = g_wrapper_kind;
+    return g_wrapper_kind < 0 ? -1 : 0;
+}
+
+MH_API int KernelReleaseCache(void) {
+    int current = 0;
+    const bool have = hipGetDevice(&current) == hipSuccess;
+    const int freed = release_pools();
+    if (have) (void)hipSetDevice(current);
+    return freed;
+}
 
 MH_API int KernelEvaluateCosts(const relationshipStruct* rss, const relationshipAngleStruct* rsa,
                                const positionAndRotation* cfgs, int n_cfgs,

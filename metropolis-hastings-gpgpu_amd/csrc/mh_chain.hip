@@ -1819,8 +1819,15 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         }
     } else {  // OP_FINAL / OP_EVAL: full costs including OffLimits
         ClPairs clf;
+        // (debug builds: the OffLimits boxes -- this pass's one array past the step layout -- lie
+        // inside the chain's LDS slot, and the launch's LDS covers every chain of the workgroup)
+        MH_CK(a.lay.OFF >= F.end && a.lay.OFF + 16 * n <= a.lay.stride, 16, a.lay.OFF, a.lay.stride);
         eval_costs<L, NPL, true, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, clf, clf);
-        if (r == 0) {
+        // Output slot: in [0, n_chains) (tempering: a rung of the chain's own group)
+        const int64_t oi = out_index(a, chain);
+        const bool oi_ok = MH_CK(oi >= 0 && oi < a.n_chains && oi / a.n_temps == chain / a.n_temps,
+                                 14, (unsigned)oi, (unsigned)chain);
+        if (r == 0 && oi_ok) {
             resultCosts rc;
             rc.totalCosts = cur[0];
             rc.PairWiseCosts = cur[1];
@@ -1830,13 +1837,13 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             rc.ClearanceCosts = cur[5];
             rc.OffLimitsCosts = cur[6];
             rc.SurfaceAreaCosts = cur[7];
-            a.costs[out_index(a, chain)] = rc;
+            a.costs[oi] = rc;
         }
         if constexpr (OP == OP_FINAL) {
 #pragma unroll
             for (int m = 0; m < NPL; ++m) {
                 const int i = m * L + r;
-                if (i >= n) break;
+                if (i >= n || !oi_ok) break;
                 point p;
                 p.x = (float)op.x[m];
                 p.y = (float)op.y[m];
@@ -1844,7 +1851,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 p.rotX = (float)ch.zrr[n + i];
                 p.rotY = (float)op.ry[m];
                 p.rotZ = (float)ch.zrr[2 * n + i];
-                a.pts[out_index(a, chain) * (int64_t)n + i] = p;
+                a.pts[oi * (int64_t)n + i] = p;
             }
         }
     }

@@ -7,10 +7,12 @@ the reference edges that short runs do not reach -- each chain bit for bit again
 * config 3: 256 chains sampled by global id out of a 65,536-chain, 100k-step session (the
   bench's own session: same room, seed and length), plus the device summary of all 65,536
   chains (the bench's mean_final_cost) against the downloaded costs;
-* config 4: one rank's shard (global ids 7*65,536 ...), the 2-rank bench.py launcher path, and
-  KernelWrapper's in-process $MH_DEVICES sharding (unmeasured on 8 GPUs: the driver runs those);
+* config 4: one rank's shard (global ids 7*65,536 ...) at 5k steps, every one of the 524,288
+  global ids of the 8 shards at 20 steps, the bench.py launcher path (2 gloo ranks, and one
+  nccl rank whose RCCL all-gather really executes), and KernelWrapper's in-process $MH_DEVICES
+  sharding (unmeasured on 8 GPUs: the driver runs those);
 * config 5: 64 chains sampled out of a 32,768-chain, 10k-step session of the 256-object room;
-* every chain of configs 3, 4 (rank 7's shard) and 5 at 20 steps: the whole population's
+* every chain of configs 3, 4 (all 8 shards) and 5 at 20 steps: the whole population's
   workgroup slots and global id -> Philox subsequence mapping, not a sample;
 * the index-n pick (u == 1.0f, Kernel.cu:566-574,598-602) on every RNG path, from a searched
   fixture (tests/golden/find_index_n.py);
@@ -35,7 +37,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from parity_util import ParityReport, check_chains
+from parity_util import ParityReport, check_chains, forked_chains
 
 pytestmark = pytest.mark.gpu
 
@@ -176,7 +178,6 @@ def test_config4_rank7_shard(mh, orc, hiplib):
 
 @pytest.mark.parametrize("name,n,chains,offset", [
     ("config 3", 64, 65536, 0),
-    ("config 4 rank-7 shard", 64, 65536, 7 * 65536),
     ("config 5", 256, 32768, 0)])
 def test_every_chain_short(mh, orc, hiplib, name, n, chains, offset):
     """Every chain of a config's full population, at 20 steps: each workgroup slot, wavefront
@@ -198,6 +199,92 @@ def test_every_chain_short(mh, orc, hiplib, name, n, chains, offset):
                  pts, costs, ref_pts, ref_costs, ids=offset + np.arange(chains), report=True)
     assert summ.accepted == int(np.asarray(ref_acc).sum())
     _check_summary(f"{name} ({steps} steps)", summ, costs, offset=offset)
+
+
+def test_config4_every_chain_all_shards(mh, orc, hiplib):
+    """Config 4's whole population: all 524,288 global ids, as the 8 ranks of the 8-GPU run
+    shard them (rank r: a 65,536-chain session with chain_offset r * 65,536, Kernel.cu:950 one
+    block per chain), run one after another on this GPU for 20 steps and compared chain by chain
+    with the oracle at the same global ids. Each shard's device summary (what bench.py
+    all-gathers) is checked against its downloaded costs, and the combined record
+    (bench.combine_records) against the whole population's."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    room = mh.synthetic_room(64)
+    per, ranks, steps, seed = 65536, 8, 20, 42
+    forked, compared, recs = 0, 0, []
+    dev_sum = ref_sum = 0.0
+    best = (-np.inf, -1)
+    for r in range(ranks):
+        off = r * per
+        with mh.Session(room, per, seed=seed, chain_offset=off) as s:
+            s.run(steps)  # (queued; the oracle runs meanwhile)
+            with _fast_oracle(orc):
+                ref_pts, ref_costs, ref_acc = orc.run_chains(room, per, steps, seed,
+                                                             chain_begin=off,
+                                                             threads=HOST_THREADS)
+            s.finalize()
+            pts, costs = s.download()
+            summ = s.summary()
+        bad = forked_chains(pts, costs, ref_pts, ref_costs)
+        assert len(bad) == 0, (f"config 4 rank {r}: {len(bad)} of {per} chains forked (global "
+                               f"ids {(off + bad[:32]).tolist()})")
+        forked += len(bad)
+        compared += per
+        assert summ.accepted == int(np.asarray(ref_acc).sum())
+        _check_summary(f"config 4 rank {r} ({steps} steps)", summ, costs, offset=off)
+        recs.append(bench.summary_record(summ.sum_total, summ.best_total, summ.best_chain,
+                                         summ.n_chains, summ.accepted))
+        dev_sum += float(costs[:, 0].astype(np.float64).sum())
+        ref_sum += float(np.asarray(ref_costs)[:, 0].astype(np.float64).sum())
+        k = int(np.argmax(costs[:, 0]))
+        if costs[k, 0] > best[0]:
+            best = (float(costs[k, 0]), off + k)
+    job = bench.combine_records(recs)
+    assert job["chains"] == compared == ranks * per
+    assert (job["best_final_cost"], job["best_chain"]) == best
+    mean, ref_mean = dev_sum / compared, ref_sum / compared
+    assert job["mean_final_cost"] == pytest.approx(mean, rel=1e-12)
+    rel = abs(mean - ref_mean) / abs(ref_mean)
+    assert rel <= 1e-4
+    warnings.warn(f"config 4 (N=64, all {compared} chains of the 8 shards x {steps} steps, global "
+                  f"ids 0..{compared - 1}): {forked} of {compared} chains forked; mean final "
+                  f"total {mean:.9g} vs oracle {ref_mean:.9g} (rel {rel:.3g}); combined record "
+                  f"best {best[0]:.9g} at chain {best[1]}", ParityReport)
+
+
+def test_config4_rccl_all_gather_single_gpu(mh, hiplib, tmp_path):
+    """The RCCL leg of bench.py executed for real on this box's one GPU: torch.distributed.run
+    with one rank, backend nccl, `--collective` lifting the world-size gate, so the communicator
+    is created and the summary records are all-gathered as device tensors. The line must name
+    the nccl backend, and its record must equal one Session's (unmeasured on 8 GPUs)."""
+    n, per, iters, steps, warmup, seed = 16, 4096, 100, 2, 1, 42
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("MH_BENCH_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(ROOT / "bench.py"), "--gpus", "1", "--collective", "--objects", str(n),
+           "--chains", str(per), "--iters", str(iters), "--steps", str(steps), "--warmup",
+           str(warmup), "--seed", str(seed), "--no-cpu-baseline", "--e2e-iters", "0"]
+    out = subprocess.run(cmd, env=env, cwd=tmp_path, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    d = rec["distributed"]
+    assert d["backend"] == "nccl" and d["world_size"] == 1 and d["distinct_gpus"] == 1
+    assert [x["rank"] for x in d["ranks"]] == [0]
+    room = mh.synthetic_room(n)
+    with mh.Session(room, per, seed=seed) as s:
+        s.run((steps + warmup) * iters)
+        s.finalize()
+        summ = s.summary()
+    assert rec["best_chain"] == summ.best_chain
+    assert rec["best_final_cost"] == float(summ.best_total)
+    assert rec["accepted"] == summ.accepted
+    assert rec["mean_final_cost"] == pytest.approx(summ.sum_total / per, rel=1e-12)
+    warnings.warn(f"RCCL all-gather executed: backend {d['backend']}, world size "
+                  f"{d['world_size']}, rank 0 on device {d['ranks'][0]['device']} (PCI bus "
+                  f"{d['ranks'][0]['pci_bus']}); record equals one Session's", ParityReport)
 
 
 def _free_port():
@@ -434,3 +521,36 @@ def test_kernelwrapper_pooled_sessions(mh, orc, hiplib):
             first = (pts, costs)
         elif (n, chains, steps, seed, kw) == calls[0]:
             assert np.array_equal(pts.view(np.uint32), first[0].view(np.uint32))
+
+
+def test_kernelwrapper_pool_follows_overrides(mh, orc, hiplib, monkeypatch):
+    """A pooled session keeps its kernel choice only while the tuning overrides are unchanged
+    (ADVICE round 5): two calls of the same room shape and chain count, one under $MH_SPEC=1 and
+    one under $MH_SPEC=0, must run different step kernels (and give the same chains); likewise
+    $MH_LANES. KernelReleaseCache() then frees the idle sessions, and the next call builds a new
+    one with the same result."""
+    room = mh.synthetic_room(8)
+    chains, steps, seed = 512, 200, 77
+    rp, rc, _ = orc.run_chains(room, chains, steps, seed, threads=HOST_THREADS)
+    got = {}
+    for spec in ("1", "0"):
+        monkeypatch.setenv("MH_SPEC", spec)
+        pts, costs = mh.kernel_wrapper(room, chains, steps, seed=seed)
+        got[spec] = mh.wrapper_step_kernel()
+        check_chains(f"pooled KernelWrapper MH_SPEC={spec}", pts, costs, rp, rc)
+    assert got["1"][1] == "speculative" and got["0"][1] != "speculative"
+    monkeypatch.setenv("MH_SPEC", "0")
+    room64 = mh.synthetic_room(64)
+    rp, rc, _ = orc.run_chains(room64, 64, 50, seed, threads=HOST_THREADS)
+    lanes = []
+    for want in ("64", "32"):
+        monkeypatch.setenv("MH_LANES", want)
+        monkeypatch.setenv("MH_DELTA", "0")
+        pts, costs = mh.kernel_wrapper(room64, 64, 50, seed=seed)
+        lanes.append(mh.wrapper_step_kernel()[0])
+        check_chains(f"pooled KernelWrapper MH_LANES={want}", pts, costs, rp, rc)
+    assert lanes == [64, 32]
+    assert mh.release_cache() >= 1
+    assert mh.release_cache() == 0
+    pts, costs = mh.kernel_wrapper(room64, 64, 50, seed=seed)
+    check_chains("KernelWrapper after KernelReleaseCache", pts, costs, rp, rc)

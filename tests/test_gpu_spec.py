@@ -102,11 +102,15 @@ def test_spec_is_the_default_for_few_small_chains(mh, hiplib, monkeypatch):
         assert s.step_kernel()[2] != "speculative"
     with mh.Session(mh.synthetic_room(16), 1024, seed=1) as s:
         assert s.step_kernel()[2] != "speculative"
-    with mh.Session(mh.synthetic_room(8), 16384, seed=1) as s:  # 64 per CU on 256 CUs
+    # the cutoff is 64 chains per CU of this device (16,384 on MI355X's 256 CUs; another SKU or
+    # a compute-partition mode moves it)
+    import torch
+    cut = 64 * torch.cuda.get_device_properties(0).multi_processor_count
+    with mh.Session(mh.synthetic_room(8), cut, seed=1) as s:
         assert s.step_kernel()[2] == "speculative"
-    with mh.Session(mh.synthetic_room(8), 16385, seed=1) as s:
+    with mh.Session(mh.synthetic_room(8), cut + 1, seed=1) as s:
         assert s.step_kernel()[2] != "speculative"
-    with mh.Session(mh.synthetic_room(8), 1 << 16, seed=1) as s:  # enough chains to fill the GPU
+    with mh.Session(mh.synthetic_room(8), max(1 << 16, 2 * cut), seed=1) as s:  # fills the GPU
         assert s.step_kernel()[2] != "speculative"
     monkeypatch.setenv("MH_SPEC", "0")
     with mh.Session(mh.synthetic_room(8), 1024, seed=1) as s:

@@ -26,7 +26,9 @@ SITES = {20: "certain REJECT but Accept accepts", 21: "certain ACCEPT but Accept
          30: "a FocalPoint estimate outside kDeltaCph",
          31: "a PairWise estimate outside kPwEstU U",
          32: "a PairWiseAngle estimate outside its allowance",
-         33: "a deferred Symmetry row maximum outside its estimate's allowance"}
+         33: "a deferred Symmetry row maximum outside its estimate's allowance",
+         14: "the final pass's output slot outside [0, n_chains)",
+         16: "the final pass's OffLimits boxes outside the chain's LDS slot"}
 
 # (room kind, N, chains, steps, kernel): the configs' rooms and edge rooms; "wild" moves every
 # object far outside the proven symmetry range, "negw" flips the weights' signs.
@@ -36,12 +38,17 @@ CASES = [("syn", 64, 8192, 2000, "full"), ("syn", 256, 2048, 1500, "incremental"
          ("wrap", 64, 2048, 2000, "full"), ("manyrel", 200, 1024, 1000, "incremental"),
          ("wrap", 256, 1024, 1000, "incremental"),
          ("negw", 64, 2048, 2000, "full"), ("negw", 256, 1024, 1000, "incremental"),
-         ("wild", 64, 1024, 1000, "full"), ("wild", 256, 512, 500, "incremental")]
+         ("wild", 64, 1024, 1000, "full"), ("wild", 256, 512, 500, "incremental"),
+         # the round-5 download fault's test shape (test_bound_decision_paths[main-32]): the
+         # console harness's room, current costs read, then the final pass (index-checked)
+         ("main", 32, 512, 600, "full"), ("main", 32, 512, 600, "incremental")]
 
 
 def room_of(mh, kind, n):
     if kind == "manyrel":  # more relationships than objects (R > N + 1)
         return mh.synthetic_room(n, n_rel=3 * n + 5)
+    if kind == "main":
+        return mh.main_fixture()
     room = mh.synthetic_room(n)
     if kind == "wrap":  # angle ranges crossing zero: the fmodf branch of Kernel.cu:245-250
         for k in range(room.srf.nRelationships):
@@ -69,11 +76,17 @@ def one(kind, n, chains, steps, kernel):
     with mh.Session(room, chains, seed=4242 + n) as s:
         assert s.step_kernel()[2].split("-")[0] == kernel, s.step_kernel()
         s.run(steps)
+        s.current_costs()
         s.finalize()
         _, costs = s.download()
     ck = (C.c_uint * 8)()
     fn = lib.mh_debug_check_delta if kernel == "incremental" else lib.mh_debug_check
     assert fn(ck) == 0
+    if kernel == "incremental":  # (the init and final passes are the full kernel's: its record)
+        ckf = (C.c_uint * 8)()
+        assert lib.mh_debug_check(ckf) == 0
+        if ckf[0] and not ck[0]:
+            ck[0], ck[1], ck[2], ck[3] = ckf[0], ckf[1], ckf[2], ckf[3]
     dc = (C.c_ulonglong * 4)()
     fd = lib.mh_debug_decisions_delta if kernel == "incremental" else lib.mh_debug_decisions
     assert fd(dc) == 0

@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the GPU box: A/B of library variants (ablate/libmhgpu_<v>.so; "main" = the product) over
+# On the GPU box: A/B of library variants (abvar/libmhgpu_<v>.so; "main" = the product) over
 # several configs, alternated $MH_AB_REPS times so drift hits every variant. Prints value and
 # mean final cost per run (equal means across variants: the same trajectories).
 #   MH_AB_CFGS="8,1024,2000,4 64,65536,1000,3" tools/box_abn.sh <tag> <variant>...
@@ -12,7 +12,7 @@ for rep in $(seq 1 ${MH_AB_REPS:-2}); do
     set -- ${CFG//,/ } "${@}"
     N=$1; CH=$2; IT=$3; ST=$4; shift 4
     for V in "$@"; do
-      if [ "$V" = main ]; then LIB=metropolis-hastings-gpgpu_amd/libmhgpu.so; else LIB=ablate/libmhgpu_$V.so; fi
+      if [ "$V" = main ]; then LIB=metropolis-hastings-gpgpu_amd/libmhgpu.so; else LIB=abvar/libmhgpu_$V.so; fi
       F=$OUT/${V}_n${N}_$rep
       MH_LIB=$LIB timeout -k 10 240 python bench.py --objects $N --chains $CH --iters $IT --steps $ST \
           --warmup 1 --no-cpu-baseline --e2e-iters 0 > $F.json 2> $F.err || { tail -5 $F.err; exit 1; }

@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-ldsconf}; mkdir -p $OUT
 ARGS="--steps 1 --warmup 1 --iters 1000 --no-cpu-baseline --e2e-iters 0"
 for V in main 1 2 8 32; do
-  if [ "$V" = main ]; then LIB=metropolis-hastings-gpgpu_amd/libmhgpu.so; else LIB=ablate/libmhgpu_$V.so; fi
+  if [ "$V" = main ]; then LIB=metropolis-hastings-gpgpu_amd/libmhgpu.so; else LIB=abvar/libmhgpu_$V.so; fi
   MH_LIB=$LIB timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU \
       -d $OUT/pmc_$V -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/pmc_$V.log 2>&1 || { tail -5 $OUT/pmc_$V.log; exit 1; }
   python3 - "$OUT/pmc_$V" "$V" <<'PY'

@@ -7,7 +7,7 @@ TAG=${1:-variants}; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 for V in "$@"; do
-  if [ "$V" = main ]; then unset MH_LIB; else export MH_LIB=ablate/libmhgpu_$V.so; fi
+  if [ "$V" = main ]; then unset MH_LIB; else export MH_LIB=abvar/libmhgpu_$V.so; fi
   for CFG in ${MH_VARIANT_CFGS:-64,65536,1000,5}; do
     set -- ${CFG//,/ }
     timeout -k 10 300 python bench.py --objects $1 --chains $2 --iters $3 --steps $4 --warmup 1 \

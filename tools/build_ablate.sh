@@ -8,7 +8,7 @@
 # runs phase bit K twice with identical results (cost probe: the trajectory is unchanged).
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p ablate
+mkdir -p abvar
 C=metropolis-hastings-gpgpu_amd/csrc
 for M in "$@"; do
   case "$M" in
@@ -27,6 +27,6 @@ for M in "$@"; do
   esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
     -Wno-unused-result $DEF $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip $C/mh_spec.hip \
-    $C/mh_abi.cpp -o ablate/libmhgpu_$M.so &
+    $C/mh_abi.cpp -o abvar/libmhgpu_$M.so &
 done
 wait

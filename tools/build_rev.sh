@@ -1,5 +1,5 @@
 #!/bin/bash
-# Builds the product library of a git revision into ablate/libmhgpu_<name>.so (A/B timing
+# Builds the product library of a git revision into abvar/libmhgpu_<name>.so (A/B timing
 # against the working tree in one GPU call).   tools/build_rev.sh <rev> <name>
 set -e
 cd "$(dirname "$0")/.."
@@ -13,5 +13,5 @@ C=$T/metropolis-hastings-gpgpu_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
   -Wno-unused-result $C/mh_chain.hip $C/mh_chain_xw.hip $C/mh_chain_best.hip $C/mh_delta.hip \
   $(test -f $C/mh_spec.hip && echo $C/mh_spec.hip) $C/mh_abi.cpp \
-  -o ablate/libmhgpu_$NAME.so
+  -o abvar/libmhgpu_$NAME.so
 rm -rf $T

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: the speculative kernel's per-batch records (ablate/libmhgpu_specdbg.so,
+"""Diagnostic: the speculative kernel's per-batch records (abvar/libmhgpu_specdbg.so,
 MH_SPEC_DEBUG) against the sequential chain's proposals and decisions from the oracle."""
 import ctypes as C
 import os

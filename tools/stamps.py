@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase cycle shares of the step kernel from a diagnostic build with MH_STAMPS=1
-(ablate/libmhgpu_stamps.so, made by tools/build_ablate.sh stamps). Run on the GPU box:
+(abvar/libmhgpu_stamps.so, made by tools/build_ablate.sh stamps). Run on the GPU box:
     MH_LANES=32 python tools/stamps.py [objects] [chains] [iters]
 Read the SHARES, not the absolute time: the stamps' waits forbid some overlap."""
 import ctypes as C
