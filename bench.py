@@ -32,6 +32,7 @@ import __graft_entry__ as graft  # noqa: E402
 
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (== FP32 MFMA peak)
 HBM_PEAK_GBS = 8000.0
+VALU_LANE_OPS_PEAK = FP32_VECTOR_PEAK_TFLOPS * 1e12 / 2  # lane-operations/s (an FMA is 2 flops)
 STEPS_PER_LAUNCH = 1000  # the library's launch chunk (mh_abi.cpp kStepsPerLaunch)
 
 
@@ -378,6 +379,14 @@ def main() -> int:
                 # the PMC VALU wavefront instructions per chain-step of this build.
                 "executed_valu_wave_insts_per_chain_step": (
                     pmc["valu_wave_insts_per_launch"] / (args.chains * pmc["iters_per_launch"])
+                    if pmc.get("valu_wave_insts_per_launch") else None),
+                # The executed work against the same peak: VALU lane-operations (wavefront
+                # instructions x 64 lanes, from the PMC record) per second of this run's launches,
+                # over the 78.6e12 lane-ops/s the 157.3 TFLOP/s FMA peak is made of (256 CUs x
+                # 128 lanes x 2.4 GHz). `frac` counts the canonical full-recompute flops F; this
+                # counts what the kernel issues (incremental work skips, exact passes add).
+                "executed_valu_frac": (
+                    pmc["valu_wave_insts_per_launch"] * 64 / launch_s / VALU_LANE_OPS_PEAK
                     if pmc.get("valu_wave_insts_per_launch") else None),
                 # VALU issue utilisation of the profiled launch (tools/pmc_summary.py): busy
                 # SIMD cycles priced per instruction class / (1024 SIMDs x kernel cycles)

@@ -16,6 +16,7 @@
 #   prof=N,chains,iters,steps    tools/profile_box.sh: kernel trace + the PMC passes
 #   bound                tools/bound_check.py (every room, full length)
 #   stamps=N,chains,iters        tools/stamps.py on abvar/libmhgpu_stamps.so
+#   spread=N,chains,launches,iters  tools/launch_spread.py (per-launch time and bound decisions)
 # Example:
 #   gpurun --timeout 1200 -- 'bash tools/box.sh r06a suite smoke bench=64,65536,1000,3'
 set -o pipefail
@@ -66,6 +67,11 @@ for STEP in "$@"; do
       MH_LIB=abvar/libmhgpu_stamps.so timeout -k 10 300 python tools/stamps.py $1 $2 $3 \
           > "$OUT/stamps_n$1.txt" 2>&1 || { tail -10 "$OUT/stamps_n$1.txt"; exit 1; }
       tail -25 "$OUT/stamps_n$1.txt" ;;
+    spread)  # tools/launch_spread.py: per-launch time beside the check build's decision counts
+      set -- ${VAL//,/ }
+      timeout -k 10 600 python tools/launch_spread.py $1 $2 $3 $4 > "$OUT/spread_n$1.txt" 2>&1 \
+          || { tail -20 "$OUT/spread_n$1.txt"; exit 1; }
+      cat "$OUT/spread_n$1.txt" ;;
     *) echo "box.sh: unknown step '$STEP'"; exit 2 ;;
   esac
 done

@@ -14,7 +14,7 @@ import __graft_entry__ as graft  # noqa: E402
 
 os.environ["MH_SPEC"] = "1"
 mh, orc = graft.load_package(), graft.load_oracle()
-lib = mh.load_library(str(ROOT / "ablate" / "libmhgpu_specdbg.so"))
+lib = mh.load_library(str(ROOT / "abvar" / "libmhgpu_specdbg.so"))
 mh.abi._lib = lib
 lib.mh_debug_spec.argtypes = [C.POINTER(C.c_uint), C.c_int]
 n, chain, steps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])

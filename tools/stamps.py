@@ -10,7 +10,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-os.environ.setdefault("MH_LIB", str(ROOT / "ablate" / "libmhgpu_stamps.so"))
+os.environ.setdefault("MH_LIB", str(ROOT / "abvar" / "libmhgpu_stamps.so"))
 import __graft_entry__ as graft  # noqa: E402
 
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
