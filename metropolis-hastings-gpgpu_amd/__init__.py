@@ -7,7 +7,7 @@ bench use. The directory name contains hyphens, so load it with load_package() b
 importlib) rather than a plain import.
 """
 from .abi import (COST_FIELDS, EXPORTS, LIB_PATH, MHError, Room, Session, STRUCT_LAYOUT,  # noqa: F401
-                  debug_collectives, debug_math, debug_rng, evaluate_costs, kernel_wrapper,
+                  debug_collectives, debug_math, device_cus, debug_rng, evaluate_costs, kernel_wrapper,
                   last_error, load_library, MH_PROBE_COUNT, probe_width, release_cache,
                   wrapper_step_kernel)
 from .rooms import clone_cfg, main_fixture, synthetic_room  # noqa: F401

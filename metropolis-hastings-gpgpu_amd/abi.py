@@ -314,6 +314,20 @@ def kernel_wrapper(room: Room, chains: int, iterations: int, seed: int | None = 
 STEP_KINDS = {0: "full", 1: "incremental", 2: "full-few", 3: "speculative"}
 
 
+HIP_ATTR_MULTIPROCESSOR_COUNT = 63  # hipDeviceAttributeMultiprocessorCount (ROCm 7.2 headers)
+
+
+def device_cus(device: int = 0) -> int:
+    """Compute units of a HIP device, asked of the HIP runtime libmhgpu.so uses (not torch's:
+    a test process that has already initialised that runtime must not initialise a second)."""
+    load_library()
+    hip = C.CDLL("libamdhip64.so.7")
+    v = C.c_int()
+    if hip.hipDeviceGetAttribute(C.byref(v), HIP_ATTR_MULTIPROCESSOR_COUNT, device) != 0:
+        raise MHError("hipDeviceGetAttribute failed")
+    return v.value
+
+
 def wrapper_step_kernel():
     """(lanes per chain, kind) of the step kernel this thread's last kernel_wrapper call ran."""
     lib = load_library()

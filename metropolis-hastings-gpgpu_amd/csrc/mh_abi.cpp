@@ -231,6 +231,7 @@ struct Geometry {
     int L, npl, waves;   // full-evaluation kernel (init, final, evaluation; step when !delta)
     bool few;            // step with OP_STEP_FEW (no register cap: too few chains to use it)
     bool spec;           // step with the speculative kernel (mh_spec.hip)
+    int spec_h;          // its halves: 2 (16-node tree, 4 wavefronts per chain) or 1 (8, 2)
     mh::ChainLds lay;    // init / step
     int waves_ol;
     mh::ChainLds lay_ol; // final / evaluation (with the OffLimits boxes)
@@ -322,6 +323,15 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
     g.spec = plain && mh::spec_fits(n, c, r) && n_chains <= 64LL * cus;
     if (const char* e = getenv("MH_SPEC"))
         if (*e) g.spec = plain && mh::spec_fits(n, c, r) && atoi(e) != 0;
+    // At most two chains per CU (at most two of a chain's four wavefronts per SIMD), the 16-node
+    // tree: 4.1 steps per batch instead of 3.2 for a batch ~21% longer. More chains share the
+    // SIMDs, and the longer batch costs more than the steps gain. Measured at N = 8, ms per
+    // 1,000-step launch, 8-node (H = 1) / 16-node (H = 2) tree (profiles/r06/r06e_spec_halves_ab.txt):
+    // 256 chains 1.67 / 1.55, 512 chains 1.83 / 1.78, 1,024 chains (config 2) 1.93 / 2.28.
+    // $MH_SPEC_H=1/2 forces the halves.
+    g.spec_h = n_chains <= 2LL * cus ? 2 : 1;
+    if (const char* e = getenv("MH_SPEC_H"))
+        if (*e) g.spec_h = atoi(e) >= 2 ? 2 : 1;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
     g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
@@ -536,7 +546,7 @@ bool record_done(mh_session* s, hipStream_t st) {
 // made after one of them changed runs the kernel it names, not the previous call's.
 std::string geometry_env() {
     static const char* const kVars[] = {"MH_LANES", "MH_WAVES", "MH_STEP_FEW", "MH_SPEC",
-                                        "MH_DELTA", "MH_DELTA_WAVES"};
+                                        "MH_SPEC_H", "MH_DELTA", "MH_DELTA_WAVES"};
     std::string key;
     for (const char* v : kVars) {
         const char* e = getenv(v);
@@ -612,7 +622,7 @@ bool session_run(mh_session* s, int iterations, hipStream_t st) {
         if (s->n_temps > 1)  // stop at the next exchange round
             chunk = (int)std::min<int64_t>(chunk, s->swap_interval - s->steps_done % s->swap_interval);
         a.iterations = chunk;
-        if (s->geo.spec) MH_TRY_HIP(mh::launch_spec(a, st));
+        if (s->geo.spec) MH_TRY_HIP(mh::launch_spec(a, s->geo.spec_h, st));
         else if (s->geo.delta) MH_TRY_HIP(mh::launch_delta(a, s->geo.dwaves, st));
         else MH_TRY_HIP(mh::launch(s->geo.few ? mh::OP_STEP_FEW : mh::OP_STEP, a, s->geo.L,
                                    s->geo.npl, s->geo.waves, st));
@@ -1241,7 +1251,8 @@ MH_API int mh_session_geometry(const mh_session* s, int* lanes_per_chain, int* c
     if (!s) { set_error("NULL session"); return -1; }
     const int L = (s->geo.delta || s->geo.spec) ? 64 : s->geo.L;  // the step kernel's shape
     const int w = s->geo.spec ? mh::spec_waves() : s->geo.delta ? s->geo.dwaves : s->geo.waves;
-    if (lanes_per_chain) *lanes_per_chain = s->geo.spec ? 64 * mh::spec_waves_per_chain() : L;
+    if (lanes_per_chain)
+        *lanes_per_chain = s->geo.spec ? 64 * mh::spec_waves_per_chain(s->geo.spec_h) : L;
     if (chains_per_workgroup) *chains_per_workgroup = w * (64 / L);
     if (incremental) *incremental = s->geo.spec ? 3 : s->geo.delta ? 1 : (s->geo.few ? 2 : 0);
     return 0;
@@ -1252,7 +1263,7 @@ MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
     const auto& g = s->geo;
     int blocks = 0;
     if (g.spec) {
-        *chains_per_cu = mh::spec_blocks_per_cu() * mh::spec_waves();
+        *chains_per_cu = mh::spec_blocks_per_cu(g.spec_h) * mh::spec_waves();
     } else if (g.delta) {
         blocks = mh::delta_blocks_per_cu(s->room.rm.n, g.dwaves,
                                          mh::delta_lds_bytes(s->geo.dlay, g.dwaves));

@@ -66,14 +66,14 @@ hipError_t launch_rng(int kind, uint64_t seed, uint64_t subsequence, int n, unsi
                       float* uni, float* nrm, hipStream_t s);
 hipError_t launch_exchange(const LaunchArgs& a, int* perm, int round, hipStream_t s);
 hipError_t launch_math(int fn, uint64_t start, uint64_t count, double* out, hipStream_t s);
-// The speculative step kernel (mh_spec.hip): rooms of at most 8 objects and 16 relationships,
-// one chain per wavefront evaluating 8 consecutive proposals at once.
+// The speculative step kernel (mh_spec.hip): rooms of at most 8 objects and 16 relationships;
+// a chain's 2 * halves wavefronts evaluate a tree of 8 * halves proposal histories at once.
 bool spec_fits(int n, int c, int r);
-int spec_waves();            // chains per workgroup of the speculative kernel
-int spec_waves_per_chain();  // its wavefronts per chain
-size_t spec_lds_bytes(int waves_per_wg);
-int spec_blocks_per_cu();
-hipError_t launch_spec(const LaunchArgs& a, hipStream_t s);
+int spec_waves();                       // chains per workgroup of the speculative kernel
+int spec_waves_per_chain(int halves);   // its wavefronts per chain
+size_t spec_lds_bytes(int halves);
+int spec_blocks_per_cu(int halves);
+hipError_t launch_spec(const LaunchArgs& a, int halves, hipStream_t s);
 hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
                               hipStream_t s);
 

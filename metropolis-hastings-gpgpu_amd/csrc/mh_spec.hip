@@ -3,18 +3,16 @@
 //
 // A chain's draws do not depend on its accept decisions: the object pick redraws on the static
 // frozen flags only (Kernel.cu:598-602), Box-Muller's cached second normal advances with the
-// draws alone, and Accept draws its uniform on every step (:710). So the proposals of steps
-// t .. t+7 are known before any of them is decided. One chain owns a workgroup of two
-// wavefronts; the 64 lanes of each are K = 8 groups of GL = 8 lanes, and group g holds a copy of
-// the current configuration (lane r: object r) and evaluates proposal t + g against it (wave 0
-// the exact FocalPoint and relationship terms, wave 1 symmetry and the Clearance / SurfaceArea
-// lists, each replaying its own sums) exactly as the reference does (Costs(),
-// Kernel.cu:516-550, every sum in the reference's order). Steps t .. t+g*-1 before the first
-// accepted proposal g* are rejections, which leave the configuration unchanged, so group g*'s
-// evaluation is exactly the sequential chain's: the batch commits steps t .. t+g* and every
-// group adopts group g*'s configuration; a batch without an acceptance commits all its steps.
-// The result is the sequential chain bit for bit (every decision is Accept's on exact costs);
-// at config 2's ~41% acceptance a batch commits ~2.4 steps for about one step's latency.
+// draws alone, and Accept draws its uniform on every step (:710). So the proposals of the
+// next steps are known before any of them is decided. One chain owns a workgroup of two
+// or four wavefronts; the 64 lanes of each are K = 8 groups of GL = 8 lanes, and each group holds
+// a copy of a configuration (lane r: object r) and evaluates one node of a tree of accept /
+// reject histories (below) exactly as the reference does (Costs(), Kernel.cu:516-550, every sum
+// in the reference's order): a chain wavefront the exact FocalPoint and relationship terms, a
+// list wavefront symmetry and the Clearance / SurfaceArea lists, each replaying its own sums.
+// The realised path through the tree commits; the result is the sequential chain bit for bit
+// (every decision is Accept's on exact costs). At config 2's ~41% acceptance a 16-node batch
+// commits ~4.1 steps for about one step's latency.
 
 #include <stdint.h>
 
@@ -42,16 +40,18 @@ namespace mh {
 namespace {
 
 constexpr int GL = 8;          // lanes per group: the largest room this kernel serves
-constexpr int K = 8;           // groups: proposals evaluated per batch
+constexpr int K = 8;           // groups per wavefront: tree nodes one wavefront evaluates
 constexpr int RMAX = 2 * GL;   // relationship slots (two per lane)
-// Two wavefronts per chain (one workgroup): both locate and apply the batch's proposals; wave 0
-// then evaluates the exact FocalPoint and relationship terms and replays their sums, wave 1 the
-// symmetry rows and the Clearance / SurfaceArea lists and replays theirs; one workgroup barrier
-// hands the eight sums over. At one chain per SIMD (config 2) the step is latency-bound, and the
-// split both halves that critical path and puts two wavefronts on every SIMD.
-constexpr int kSplit = 2;      // wavefronts per chain
-constexpr int kSpecWaves = kSplit;
-
+constexpr int kNone = 31;      // "no node": the batch's incoming state, or no child
+// A chain owns a workgroup of 2H wavefronts in H halves. Half h evaluates nodes K*h .. K*h+7 of
+// the batch's tree: its chain wavefront (2h) applies each node's history, evaluates the exact
+// FocalPoint and relationship terms and replays their sums, its list wavefront (2h+1) the
+// symmetry rows and the Clearance / SurfaceArea lists and theirs; one workgroup barrier hands
+// the eight sums of every node over, and both chain wavefronts (which hold the chain's state
+// identically) decide the same realised path. At one chain per SIMD (config 2) the step is
+// latency-bound: the split halves that critical path, and H = 2 (16 nodes, launches of at most
+// four chains per CU) commits more steps per batch for about the same latency as H = 1 (8 nodes,
+// two wavefronts, seven chains per CU).
 // Each group's ordered-sum streams (doubles, pre-signed so that every sum is acc + term). Wave 0's:
 // VisualBalance area x and area y (Kernel.cu:200-201), FocalPoint -cos(phi) (:277), PairWise and
 // PairWiseAngle (:222, :249-253).
@@ -80,25 +80,26 @@ __device__ __forceinline__ int rec_k1(int code) { return ((code >> 2) & 15) - 1;
 __device__ __forceinline__ int rec_k2(int code) { return ((code >> 6) & 15) - 1; }
 __device__ __forceinline__ int rec_h(int code) { return (code >> 10) & 1; }
 
-struct SpecW0 {  // LDS of wave 0, which holds the chain
+struct SpecW0 {  // LDS of a half's chain wavefront
     double S[K][S_W0];            // each group's streams
     double RY[K][GL];             // each group's double rotY of every object (Symmetry, :305)
     double XD[K][GL], YD[K][GL];  // each group's double x, y (wave 1's symmetry and boxes)
     ObjP P[K][GL];                // each group's float pose words
 };
 
-struct SpecW1 {  // LDS of wave 1
+struct SpecW1 {  // LDS of a half's list wavefront
     double S[K][S_W1];       // each group's streams
     float4 CLB[K][GL];       // each group's clearance boxes at their sources (:414-415)
-    unsigned int wd[128];    // the 128-word window of the Philox stream being parsed
 };
 
-struct SpecShared {  // LDS of the chain shared by its two wavefronts
-    double SUM[2][K][8];  // each group's eight sums (double-buffered by batch parity)
-    StepRec ring[kRing];  // the step records (wave 1 writes, wave 0 reads)
+template <int H>
+struct SpecShared {  // LDS of the chain shared by its wavefronts
+    double SUM[2][K * H][8];  // each node's eight sums (double-buffered by batch parity)
+    StepRec ring[kRing];  // the step records (wave 1 writes, the chain wavefronts read)
+    unsigned int wd[128];  // the 128-word window of the Philox stream being parsed (wave 1)
     unsigned int produced;  // records written so far (wave 1; read by wave 0 between the barriers)
     unsigned int consumed;  // records committed so far (wave 0; read by wave 1 between them)
-    int stop;             // wave 0 to wave 1: the chain's steps are done
+    int stop;             // wave 0 to the others: the chain's steps are done
 };
 
 struct SpecHdr {  // LDS of the workgroup: the room tables
@@ -107,14 +108,17 @@ struct SpecHdr {  // LDS of the workgroup: the room tables
     RelConst rel[RMAX];
 };
 
-constexpr int kSpecHdrBytes = (int)((sizeof(SpecHdr) + 15) & ~(size_t)15);
-constexpr int kSpecW0Bytes = (int)((sizeof(SpecW0) + 15) & ~(size_t)15);
-constexpr int kSpecW1Bytes = (int)((sizeof(SpecW1) + 15) & ~(size_t)15);
-constexpr int kSpecSharedBytes = (int)((sizeof(SpecShared) + 15) & ~(size_t)15);
-// (per chain 22.1 KB with the 1.7 KB room tables: seven chains in a CU's 160 KB; round 4's two
-// full-size wave records took 37.5 KB, four chains per CU)
+constexpr int round16s(size_t v) { return (int)((v + 15) & ~(size_t)15); }
+constexpr int kSpecHdrBytes = round16s(sizeof(SpecHdr));
+constexpr int kSpecW0Bytes = round16s(sizeof(SpecW0));
+constexpr int kSpecW1Bytes = round16s(sizeof(SpecW1));
+// LDS per chain: H = 1 22.1 KB (seven chains in a CU's 160 KB), H = 2 37.1 KB (four)
+template <int H>
+constexpr int spec_bytes() {
+    return kSpecHdrBytes + H * (kSpecW0Bytes + kSpecW1Bytes) + round16s(sizeof(SpecShared<H>));
+}
 static_assert(sizeof(StepRec) == 32, "StepRec");
-constexpr int kSpecBytes = kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes + kSpecSharedBytes;
+static_assert(spec_bytes<2>() * 4 <= 160 * 1024, "four 16-node chains per CU");
 
 // A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
 __device__ __attribute__((noinline)) unsigned int philox_far(uint64_t seed, uint64_t sub,
@@ -209,91 +213,69 @@ __device__ __forceinline__ void append4(const Staged<double>& S, int& pos, float
 }
 
 // ---- speculation trees ----------------------------------------------------------------------
-// A batch evaluates the K nodes of a prefix-closed tree of accept / reject histories. Node g
-// (group g) evaluates the proposal of step t + dep(g) against the configuration its history
-// leaves -- the batch's incoming state with the proposals of the steps it accepted applied in
-// order -- and its Accept compares with the total of the node whose proposal that configuration
-// is (cpar), or the incoming total. The realised path walks from the root by Accept's decisions
-// until it leaves the tree; its steps commit. Every decision on the path is Accept's on exact
-// costs of the configuration the sequential chain holds there, so any prefix-closed tree gives
-// the sequential chain bit for bit; the shape only sets how many steps a batch commits: with
-// acceptance rate p, the sum of its nodes' path probabilities, largest for the K most probable
-// histories. (Round 4's linear speculation is the all-reject path; at config 2's p = 0.41 it
-// commits 2.46 steps per batch, the tree {root, R, A, RR, RA, AR, RRR, AA} 3.22.)
-struct SpecTree {
-    uint32_t dep;       // 4 bits per node: its step's offset in the batch
-    uint64_t hist;      // 8 bits per node: bit i set = step t + i accepted on its history
-    uint32_t cpar;      // 4 bits per node: the node whose configuration is its current one
-                        // (15: the batch's incoming state)
-    uint32_t cha, chr;  // 4 bits per node: the next node on an accept / a reject (15: none)
-    int maxdep;
+// A batch evaluates the NN nodes of a prefix-closed tree of accept / reject histories. Node k
+// evaluates the proposal of step t + dep(k) against the configuration its history leaves -- the
+// batch's incoming state with the proposals of the steps it accepted applied in order -- and its
+// Accept compares with the total of the node whose proposal that configuration is (cpar), or the
+// incoming total. The realised path walks from the root by Accept's decisions until it leaves the
+// tree; its steps commit. Every decision on the path is Accept's on exact costs of the
+// configuration the sequential chain holds there, so any prefix-closed tree gives the sequential
+// chain bit for bit; the shape only sets how many steps a batch commits: with acceptance rate p,
+// the sum of its nodes' path probabilities, largest for the NN most probable histories. (Round
+// 4's linear speculation is the all-reject path; at config 2's p = 0.41 it commits 2.46 steps per
+// batch, the 8-node tree {root, R, A, RR, RA, AR, RRR, AA} 3.22, the 16-node tree 4.14.)
+struct SpecTree {  // lane k < NN: node k; other lanes: unused
+    int dep;     // its step's offset in the batch
+    int hist;    // bit i set: step t + i accepted on its history (i < dep)
+    int cpar;    // the node whose configuration is its current one (kNone: the incoming state)
+    int cha, chr;  // the next node on an accept / a reject (kNone: none)
+    int maxdep;  // (wave-uniform) the deepest node's dep
 };
 
-// The K most probable histories for acceptance rate p, grown best-first from the root (a child
-// is less probable than its parent, so the set is prefix-closed). Wave-uniform.
+// The NN most probable histories for acceptance rate p, grown best-first from the root (a child
+// is less probable than its parent, so the set is prefix-closed), lane k building node k: each
+// round the open child of largest probability, the lowest node and its reject child first on
+// ties.
+template <int NN>
 __device__ __forceinline__ SpecTree spec_tree(float p) {
+    static_assert(NN <= 32, "nodes");
     p = fminf(fmaxf(p, 0.02f), 0.98f);
-    float pr[K];
-    int dp[K], cp[K], ca[K], cr[K];
-    uint32_t hs[K];
-    pr[0] = 1.0f;
-    dp[0] = 0;
-    hs[0] = 0u;
-    cp[0] = ca[0] = cr[0] = 15;
-#pragma unroll
-    for (int k = 1; k < K; ++k) {
-        float best = -1.0f;
-        int bi = 0, bb = 0;
-#pragma unroll
-        for (int i = 0; i < k; ++i) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const bool open = (b ? ca[i] : cr[i]) == 15;
-                const float q = pr[i] * (b ? p : 1.0f - p);
-                const bool take = open && q > best;
-                best = take ? q : best;
-                bi = take ? i : bi;
-                bb = take ? b : bb;
-            }
-        }
-        int pdp = 0, pcp = 15;
-        uint32_t phs = 0u;
-#pragma unroll
-        for (int i = 0; i < k; ++i) {
-            if (i == bi) {
-                pdp = dp[i];
-                phs = hs[i];
-                pcp = cp[i];
-                if (bb) ca[i] = k;
-                else cr[i] = k;
-            }
-        }
-        pr[k] = best;
-        dp[k] = pdp + 1;
-        hs[k] = phs | ((uint32_t)bb << pdp);
-        cp[k] = bb ? bi : pcp;
-        ca[k] = cr[k] = 15;
-    }
+    const int lane = __lane_id();
     SpecTree t;
-    t.dep = t.cpar = t.cha = t.chr = 0u;
-    t.hist = 0ull;
-    t.maxdep = 0;
+    float pr = lane == 0 ? 1.0f : -1.0f;
+    t.dep = t.hist = 0;
+    t.cpar = t.cha = t.chr = kNone;
+#pragma unroll 1
+    for (int k = 1; k < NN; ++k) {
+        const float q0 = (lane < k && t.chr == kNone) ? pr * (1.0f - p) : -1.0f;
+        const float q1 = (lane < k && t.cha == kNone) ? pr * p : -1.0f;
+        const int b = q1 > q0 ? 1 : 0;
+        const float q = b ? q1 : q0;
+        float m = q;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        t.dep |= (uint32_t)dp[k] << (4 * k);
-        t.hist |= (uint64_t)hs[k] << (8 * k);
-        t.cpar |= (uint32_t)cp[k] << (4 * k);
-        t.cha |= (uint32_t)ca[k] << (4 * k);
-        t.chr |= (uint32_t)cr[k] << (4 * k);
-        t.maxdep = max(t.maxdep, dp[k]);
+        for (int off = 1; off < 32; off <<= 1) m = fmaxf(m, __shfl_xor(m, off, 32));
+        const float mu = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+        const uint64_t hit = __ballot(lane < k && q == mu);
+        const int bi = (int)__builtin_ctzll(hit);
+        const int bb = __builtin_amdgcn_readlane(b, bi);
+        const int pdp = __builtin_amdgcn_readlane(t.dep, bi);
+        const int phs = __builtin_amdgcn_readlane(t.hist, bi);
+        const int pcp = __builtin_amdgcn_readlane(t.cpar, bi);
+        if (lane == bi) {
+            if (bb) t.cha = k;
+            else t.chr = k;
+        }
+        if (lane == k) {
+            pr = mu;
+            t.dep = pdp + 1;
+            t.hist = phs | (bb << pdp);
+            t.cpar = bb ? bi : pcp;
+        }
     }
-    t.dep = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.dep);
-    t.hist = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(t.hist >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t.hist);
-    t.cpar = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.cpar);
-    t.cha = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.cha);
-    t.chr = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.chr);
-    t.maxdep = __builtin_amdgcn_readfirstlane(t.maxdep);
+    int md = lane < NN ? t.dep : 0;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) md = max(md, __shfl_xor(md, off, 32));
+    t.maxdep = __builtin_amdgcn_readfirstlane(md);
     return t;
 }
 
@@ -310,40 +292,49 @@ __device__ __forceinline__ int nth_bit(uint32_t m, int q) {
     return pos;
 }
 
-__global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) {
+template <int H>
+__global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
+    constexpr int NN = K * H;  // tree nodes per batch
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = __lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hf = wave >> 1;            // (wave-uniform) the half: nodes K*hf .. K*hf + 7
+    const bool chain_wave = (wave & 1) == 0;
     const int g = lane >> 3, r = lane & 7, gbase = lane & ~7;
     const DevRoom& rm = a.rm;
     const int n = rm.n, c = rm.c, nr = rm.r;
 
-    SpecHdr* H = reinterpret_cast<SpecHdr*>(lds);
+    SpecHdr* Hd = reinterpret_cast<SpecHdr*>(lds);
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         RectShape s = a.objc[i].off;
         s.pad = __float_as_int(a.objc[i].area);
-        H->objs[i] = s;
+        Hd->objs[i] = s;
     }
     for (int i = threadIdx.x; i < c; i += blockDim.x) {
         RectShape s = a.clrc[i].shape;
         s.pad = a.clrc[i].src;
-        H->clrs[i] = s;
+        Hd->clrs[i] = s;
     }
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) H->rel[i] = a.relc[i];
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) Hd->rel[i] = a.relc[i];
     __syncthreads();
 
     const int64_t chain = (int64_t)blockIdx.x;  // (the whole workgroup: one chain)
     if (chain >= a.n_chains) return;
-    SpecW0* X0 = reinterpret_cast<SpecW0*>(lds + kSpecHdrBytes);
-    SpecW1* X1 = reinterpret_cast<SpecW1*>(lds + kSpecHdrBytes + kSpecW0Bytes);
-    SpecShared* SH = reinterpret_cast<SpecShared*>(lds + kSpecHdrBytes + kSpecW0Bytes + kSpecW1Bytes);
-    const bool w0 = wave == 0;  // (wave-uniform: whose phases these are)
+    // per half: the chain wavefront's LDS, then the list wavefront's; then the shared part
+    auto X0of = [&](int h) __attribute__((always_inline)) {
+        return reinterpret_cast<SpecW0*>(lds + kSpecHdrBytes + h * kSpecW0Bytes);
+    };
+    SpecW0* X0 = X0of(hf);
+    SpecW1* X1 = reinterpret_cast<SpecW1*>(lds + kSpecHdrBytes + H * kSpecW0Bytes + hf * kSpecW1Bytes);
+    SpecShared<H>* SH = reinterpret_cast<SpecShared<H>*>(
+        lds + kSpecHdrBytes + H * (kSpecW0Bytes + kSpecW1Bytes));
     int par = 0;                 // the batch's SUM buffer
     const ChainMeta m0 = a.meta[chain];
 
-    if (!w0) {
-        // ---- Wave 1: the stream's step records ahead of wave 0, and per batch the symmetry
-        // rows and the Clearance / SurfaceArea lists of every group. It keeps no chain state.
+    if (!chain_wave) {
+        // ---- The list wavefronts: per batch the symmetry rows and the Clearance / SurfaceArea
+        // lists of their half's nodes. Wave 1 also writes the stream's step records ahead of the
+        // chain wavefronts. They keep no chain state.
         //
         // The Philox stream (key = seed, subsequence = global id), 128 words at a time: lane i
         // holds words start + i and start + 64 + i; LDS the words and the Box-Muller pairs of
@@ -354,11 +345,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         // none when h = 1, swap none. So every lane parses the steps that would start at its two
         // offsets of the window, a wave-uniform walk chains the window's steps (none of it
         // depends on a decision), and lane s writes step s's record into the ring.
+        const bool producer = hf == 0;
         unsigned int fz = 1u << n;  // frozen flags, index n frozen (a pick of n is redrawn)
         for (int i = 0; i < n; ++i) fz |= (a.objc[i].frozen != 0 ? 1u : 0u) << i;
         const uint64_t seed = a.seed, sub = (uint64_t)(a.chain_offset + chain);
         uint64_t wbase = 0;
-        Published<unsigned int> win{X1->wd};
+        Published<unsigned int> win{SH->wd};
         Published<StepRec> ringv{SH->ring};
         // Draws at a lane's own offset (every lane may read a different one).
         auto word_v = [&](unsigned int o) __attribute__((always_inline)) -> unsigned int {
@@ -496,17 +488,20 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             prod += (unsigned int)nrec;
         };
         const Staged<unsigned int> PROD{&SH->produced};
-        produce();
-        produce();
-        if (lane == 0) PROD.put(0, prod);
-        __syncthreads();  // (wave 0 starts with these records)
+        if (producer) {
+            produce();
+            produce();
+            if (lane == 0) PROD.put(0, prod);
+        }
+        __syncthreads();  // (the chain wavefronts start with these records)
         unsigned int cons_seen = 0;  // records wave 0 had committed, as read between the barriers
         const Staged<double> Sst{X1->S[g]};
         const Staged<float4> CLBst{X1->CLB[g]};
 #pragma clang loop unroll(disable)
         for (;;) {
-            // the ring has room for a window (wave 0 reads records below cons_seen no more)
-            if (prod + (unsigned int)kRec <= cons_seen + (unsigned int)kRing) {
+            // the ring has room for a window (the chain wavefronts read records below cons_seen
+            // no more)
+            if (producer && prod + (unsigned int)kRec <= cons_seen + (unsigned int)kRing) {
                 produce();
                 if (lane == 0) PROD.put(0, prod);
             }
@@ -520,12 +515,12 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             float4 box = make_float4(0.f, 0.f, 0.f, 0.f), sao = box, sac = box;
             bool wild = false;
             if (r < n) {
-                box = shape_box(H->objs[r], xf, yf);
+                box = shape_box(Hd->objs[r], xf, yf);
                 sao = comp_overlaps(rm, box);  // SurfaceArea, object r (:469-480)
                 wild = !(fabs(sx) < 1e15 && fabs(sy) < 1e15 && fabs(sry) < 1e15);
             }
             if (r < c) {
-                const RectShape cs = H->clrs[r];
+                const RectShape cs = Hd->clrs[r];
                 const ObjP ps = Pg[cs.pad];
                 CLBst.put(r, shape_box(cs, ps.xf, ps.yf));      // Clearance, :414-415
                 sac = comp_overlaps(rm, shape_box(cs, xf, yf));  // SurfaceArea quirk: cfg[i], :456
@@ -554,8 +549,9 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             append4(Sst.at(S_SA), nsa, sac, r < c, r);
             append4(Sst.at(S_SA), nsa, sao, r < n, r);
             const Published<double> Sv = publish(Sst);
-            // Sums 3 (Symmetry), 4 (Clearance), 5 (SurfaceArea), as in wave 0's replay below.
-            const Staged<double> SUMst{SH->SUM[par][g]};
+            // Sums 3 (Symmetry), 4 (Clearance), 5 (SurfaceArea), as in the chain wavefronts'
+            // replay below.
+            const Staged<double> SUMst{SH->SUM[par][K * hf + g]};
             if (r >= 3 && r <= 5) {
                 const int base = r == 3 ? S_SYM : r == 4 ? S_CL : S_SA;
                 const int len = r == 3 ? n : r == 4 ? ncl : nsa;
@@ -570,9 +566,11 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         return;
     }
 
-    // ---- Wave 0: the chain ----
+    // ---- The chain wavefronts (wave 0, and wave 2 when H = 2): the same chain state in both.
     // The current configuration, in every group: lane r holds object r (z, rotX and rotZ too:
-    // no cost reads them, an accepted swap exchanges them, Kernel.cu:675-700).
+    // no cost reads them, an accepted swap exchanges them, Kernel.cu:675-700). Wave 0 alone writes
+    // the shared flags and the chain's results.
+    const bool lead = hf == 0;
     double* st = a.st + chain * (int64_t)(F_COUNT * n);
     double cx = 0.0, cy = 0.0, cry = 0.0, cz = 0.0, crx = 0.0, crz = 0.0;
     if (r < n) {
@@ -605,13 +603,13 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         Pst.put(r, p);
         RYst.put(r, cry);
     }
-    if (lane == 0) CONS.put(0, 0u);
+    if (lead && lane == 0) CONS.put(0, 0u);
     const Published<ObjP> P0 = publish(Pst);
     float cph = 0.0f;
     double rpw0 = 0.0, rang0 = 0.0, rpw1 = 0.0, rang1 = 0.0;
     if (r < n) cph = focal_cos(rm, (float)cx, (float)cy, (float)cry);
-    if (r < nr) rel_exact(H->rel[r], P0.ptr(), rpw0, rang0);
-    if (r + GL < nr) rel_exact(H->rel[r + GL], P0.ptr(), rpw1, rang1);
+    if (r < nr) rel_exact(Hd->rel[r], P0.ptr(), rpw0, rang0);
+    if (r + GL < nr) rel_exact(Hd->rel[r + GL], P0.ptr(), rpw1, rang1);
 
     __syncthreads();  // (wave 1's first records)
     const Published<StepRec> ring{SH->ring};
@@ -624,17 +622,69 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
     auto rec = [&](unsigned int i) __attribute__((always_inline)) -> const StepRec& {
         return ring[(int)(i % (unsigned int)kRing)];
     };
+    // Applies to (x, y, ry), lane r's object, the proposals of the steps i < cnt for which
+    // take(i) holds, in step order (Kernel.cu:576-704; each is the reference's edit of cfgStar,
+    // made on the configuration it would see). Every lane must be active (the swap's shuffles).
+    // The batch's records ride in registers: lane i holds record cons + i (one pair of
+    // ds_read_b128 per batch), and a step's fields are lane reads, not LDS round trips on the
+    // chain's critical path (config 2: ~750 cycles per applied step before).
+    int r_code = 0;
+    float r_d1 = 0.0f, r_d2 = 0.0f, r_u = 1.0f;
+    auto apply = [&](double& x, double& y, double& ry, bool& mv, int cnt, auto take)
+        __attribute__((always_inline)) {
+        for (int i = 0; i < cnt; ++i) {  // (wave-uniform: the step's record)
+            const bool app = take(i);
+            const int qc = __builtin_amdgcn_readlane(r_code, i);
+            const int qm = rec_mode(qc), q1 = rec_k1(qc), q2 = rec_k2(qc);
+            const float qd1 = readlane_f(r_d1, i), qd2 = readlane_f(r_d2, i);
+            if (qm == 0) {  // translate
+                if (app && r == q1) {
+                    mv = true;
+                    if (x + (double)qd1 > rm.rmax_x) x = rm.rmax_x;
+                    else if (x + (double)qd1 < rm.rmin_x) x = rm.rmin_x;
+                    else x = x + (double)qd1;
+                    if (y + (double)qd2 > rm.rmax_y) y = rm.rmax_y;
+                    else if (y + (double)qd2 < rm.rmin_y) y = rm.rmin_y;
+                    else y = y + (double)qd2;
+                }
+            } else if (qm == 1) {  // rotate
+                if (app && r == q1) {
+                    mv = true;
+                    ry = ry + (double)qd1;
+                    if (ry < 0) ry = ry + kTwoPI;
+                    else if (ry > kTwoPI) ry = ry - kTwoPI;
+                }
+            } else if (q1 >= 0) {  // swap (every lane active for the shuffles)
+                const int ia = gbase + q1, ib = gbase + q2;
+                const double ax = shfl_d(x, ia), ay = shfl_d(y, ia), ary = shfl_d(ry, ia);
+                const double bx = shfl_d(x, ib), by = shfl_d(y, ib), bry = shfl_d(ry, ib);
+                // object 1 takes object 2's pose, object 2 object 1's through float temporaries
+                if (app && r == q2) {
+                    x = (double)(float)ax;
+                    y = (double)(float)ay;
+                    ry = (double)(float)ary;
+                    mv = true;
+                } else if (app && r == q1) {
+                    x = bx;
+                    y = by;
+                    ry = bry;
+                    mv = true;
+                }
+            }
+        }
+    };
 
     unsigned int accepted = 0;
     // The batch's tree (spec_tree), rebuilt every 32 batches from this launch's acceptance rate
-    // (a prior of 2 accepts in 5 steps to start). Each lane's node is its group's.
+    // (a prior of 2 accepts in 5 steps to start): lane k < NN holds node k; each group's own
+    // node is K * hf + g.
     SpecTree tr;
-    int my_dep = 0, my_hist = 0, my_cpar = 15;
+    int my_dep = 0, my_hist = 0;
     auto set_tree = [&](float p) __attribute__((always_inline)) {
-        tr = spec_tree(p);
-        my_dep = (int)((tr.dep >> (4 * g)) & 15u);
-        my_hist = (int)((tr.hist >> (8 * g)) & 255u);
-        my_cpar = (int)((tr.cpar >> (4 * g)) & 15u);
+        tr = spec_tree<NN>(p);
+        const int src = (K * hf + g) << 2;
+        my_dep = __builtin_amdgcn_ds_bpermute(src, tr.dep);
+        my_hist = __builtin_amdgcn_ds_bpermute(src, tr.hist);
     };
     set_tree(0.4f);
     unsigned int batches = 0;
@@ -644,8 +694,8 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 #endif
 #pragma clang loop unroll(disable)
     for (int done = 0;;) {
-        if (done >= a.iterations) {  // (wave 1 leaves its loop at the same barrier)
-            if (lane == 0) STOP.put(0, 1);
+        if (done >= a.iterations) {  // (the list wavefronts leave their loop at this barrier)
+            if (lead && lane == 0) STOP.put(0, 1);
             publish_workgroup(STOP);
             break;
         }
@@ -654,53 +704,21 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         // steps this batch can reach: the tree's depth, the launch's remaining steps, the
         // records wave 1 has written (0: a round that only waits for it)
         const int kb = min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
+        if (lane < kb) {
+            const StepRec& q = rec(cons + (unsigned int)lane);
+            r_code = q.code;
+            r_d1 = q.d1;
+            r_d2 = q.d2;
+            r_u = q.u;
+        }
         SSTAMP(0);
         // Group g's configuration: the incoming state with the proposals of the steps its
-        // history accepted and then its own step's applied in step order (Kernel.cu:576-704;
-        // each is the reference's edit of cfgStar, made on the configuration it would see).
+        // node's history accepted and then its own step's applied in step order.
         double sx = cx, sy = cy, sry = cry;
         bool moved = false;  // this lane's object differs from the incoming state
-        for (int i = 0; i < kb; ++i) {  // (wave-uniform: the step's record)
-            const bool app = i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
-            const StepRec& q = rec(cons + (unsigned int)i);
-            const int qc = q.code;
-            const int qm = rec_mode(qc), q1 = rec_k1(qc), q2 = rec_k2(qc);
-            const float qd1 = q.d1, qd2 = q.d2;
-            if (qm == 0) {  // translate
-                if (app && r == q1) {
-                    moved = true;
-                    if (sx + (double)qd1 > rm.rmax_x) sx = rm.rmax_x;
-                    else if (sx + (double)qd1 < rm.rmin_x) sx = rm.rmin_x;
-                    else sx = sx + (double)qd1;
-                    if (sy + (double)qd2 > rm.rmax_y) sy = rm.rmax_y;
-                    else if (sy + (double)qd2 < rm.rmin_y) sy = rm.rmin_y;
-                    else sy = sy + (double)qd2;
-                }
-            } else if (qm == 1) {  // rotate
-                if (app && r == q1) {
-                    moved = true;
-                    sry = sry + (double)qd1;
-                    if (sry < 0) sry = sry + kTwoPI;
-                    else if (sry > kTwoPI) sry = sry - kTwoPI;
-                }
-            } else if (q1 >= 0) {  // swap (every lane active for the shuffles)
-                const int ia = gbase + q1, ib = gbase + q2;
-                const double ax = shfl_d(sx, ia), ay = shfl_d(sy, ia), ary = shfl_d(sry, ia);
-                const double bx = shfl_d(sx, ib), by = shfl_d(sy, ib), bry = shfl_d(sry, ib);
-                // object 1 takes object 2's pose, object 2 object 1's through float temporaries
-                if (app && r == q2) {
-                    sx = (double)(float)ax;
-                    sy = (double)(float)ay;
-                    sry = (double)(float)ary;
-                    moved = true;
-                } else if (app && r == q1) {
-                    sx = bx;
-                    sy = by;
-                    sry = bry;
-                    moved = true;
-                }
-            }
-        }
+        apply(sx, sy, sry, moved, kb, [&](int i) __attribute__((always_inline)) {
+            return i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
+        });
         const float xf = (float)sx, yf = (float)sy, ryf = (float)sry;
         if (r < n) {
             ObjP p;
@@ -713,9 +731,9 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             XDst.put(r, sx);
             YDst.put(r, sy);
         }
-        if (lane == 0) STOP.put(0, 0);
+        if (lead && lane == 0) STOP.put(0, 0);
         SSTAMP(1);
-        const auto pv = publish_workgroup(Pst, RYst, XDst, YDst);  // (to wave 1 as well)
+        const auto pv = publish_workgroup(Pst, RYst, XDst, YDst);  // (to the list wavefront too)
         SSTAMP(2);
         prod_seen = SH->produced;  // (wave 1 writes it before this barrier, never between)
         (void)pv;  // (the views are read below through Pall: every group's)
@@ -727,11 +745,11 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         const uint32_t mv = (uint32_t)group_ballot<GL>(moved && r < n, gbase);
         bool t0 = false, t1 = false;
         if (r < nr) {
-            const RelConst& rc = H->rel[r];
+            const RelConst& rc = Hd->rel[r];
             t0 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
         if (r + GL < nr) {
-            const RelConst& rc = H->rel[r + GL];
+            const RelConst& rc = Hd->rel[r + GL];
             t1 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
         const uint32_t tm = (uint32_t)group_ballot<GL>(t0, gbase) |
@@ -739,7 +757,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         const int nrt = __builtin_popcount(tm);
         const Staged<double> Sg = Sall.at(g * S_W0);
         if (r < n) {
-            const float area = __int_as_float(H->objs[r].pad);
+            const float area = __int_as_float(Hd->objs[r].pad);
             Sg.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
             Sg.put(S_VBY + r, (double)area * sy);
             if (!moved) Sg.put(S_FP + r, -(double)cph);
@@ -780,7 +798,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             const int idx = nth_bit(isrel ? (w & 0xffffu) : ((w >> 16) & 0xffu), isrel ? ql : ql - nrtG);
             const bool rel = has && isrel, foc = has && !isrel;
             const ObjP* PG = Pall.ptr() + G * GL;
-            const RelConst& rc = H->rel[rel ? idx : 0];
+            const RelConst& rc = Hd->rel[rel ? idx : 0];
             const ObjP qo = PG[foc ? idx : 0];
             double ay = 0.0, ax = 1.0, pw = 0.0;
             float ti = 0.0f;
@@ -804,9 +822,9 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         SSTAMP(3);
         // The eight ordered sums: lane r of each group replays stream r (float sums round every
         // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2),
-        // in the wavefront that built it (wave 1: 3, 4, 5); the workgroup barrier hands them to
-        // wave 0. The buffer alternates by batch.
-        const Staged<double> SUMst{SH->SUM[par][g]};
+        // in the wavefront that built it (the list wavefront: 3, 4, 5); the workgroup barrier
+        // hands every node's to both chain wavefronts. The buffer alternates by batch.
+        const Staged<double> SUMst{SH->SUM[par][K * hf + g]};
         if (r <= 2 || r >= 6) {
             int base = S_VBX, len = n;
             bool rnd = true;
@@ -827,12 +845,19 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         SSTAMP(4);
         const Published<double> SUMv = publish_workgroup(SUMst);
+        // (every half's streams were published by its chain wavefront before the same barrier;
+        // they are next rewritten after the next batch's views barrier)
+        auto streams_of = [&](int h) __attribute__((always_inline)) {
+            return Published<double>{&X0of(h)->S[0][0]};
+        };
         par ^= 1;
         SSTAMP(6);
-        // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547).
+        // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547), of node `lane`
+        // (lanes 0 .. NN-1; the others repeat node 0).
+        const int nd = lane < NN ? lane : 0;
         float sc[8];
         {
-            const double* sm = SUMv.ptr();
+            const double* sm = SUMv.ptr() + (nd - (K * hf + g)) * 8;  // (SUM[par][nd])
             const float nx = (float)sm[0], ny = (float)sm[1];
             const double fpd = sm[2];
             const float symf = (float)sm[3], clf = (float)sm[4], saf = (float)sm[5];
@@ -854,33 +879,43 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
         // total (the node whose configuration it started from, or the batch's incoming total).
-        const float u_g = my_dep < kb ? rec(cons + (unsigned int)my_dep).u : 1.0f;
-        const float cp_tot = shfl_f(sc[0], (my_cpar == 15 ? 0 : my_cpar) << 3);
-        const float cur_g = my_cpar == 15 ? cur[0] : cp_tot;
-        const bool acc_g = my_dep < kb && accept_u(u_g, kBeta * ((double)sc[0] - (double)cur_g));
-        const uint64_t ab = __ballot(acc_g && r == 0);
+        const float u_dep = shfl_f(r_u, tr.dep < 64 ? tr.dep : 0);  // (record dep's uniform)
+        const float u_n = tr.dep < kb ? u_dep : 1.0f;
+        const float cp_tot = shfl_f(sc[0], tr.cpar == kNone ? 0 : tr.cpar);
+        const float cur_n = tr.cpar == kNone ? cur[0] : cp_tot;
+        const bool acc_n = lane < NN && tr.dep < kb &&
+                           accept_u(u_n, kBeta * ((double)sc[0] - (double)cur_n));
+        const uint64_t ab = __ballot(acc_n);
         // The realised path from the root: its nodes' steps commit; the configuration after
         // them is the last accepted node's (or the incoming one).
-        int node = 0, steps = 0, last = 15, nacc = 0;
+        int node = 0, steps = 0, last = kNone, nacc = 0;
         unsigned int acc_steps = 0;
 #pragma unroll
-        for (int d = 0; d < K; ++d) {
-            if (node == 15 || d >= kb) break;
+        for (int d = 0; d < NN; ++d) {
+            if (node == kNone || d >= kb) break;
             ++steps;
-            const bool an = ((ab >> (node << 3)) & 1ull) != 0;
+            const bool an = ((ab >> node) & 1ull) != 0;
             if (an) {
                 last = node;
                 ++nacc;
                 acc_steps |= 1u << d;
             }
-            node = (int)(((an ? tr.cha : tr.chr) >> (4 * node)) & 15u);
+            node = __builtin_amdgcn_readlane(an ? tr.cha : tr.chr, node);
         }
-        if (last != 15) {
-            const int src = (last << 3) + r;
-            cx = shfl_d(sx, src);
-            cy = shfl_d(sy, src);
-            cry = shfl_d(sry, src);
-            const double* sl = Sv.ptr() + last * S_W0;
+        if (last != kNone) {
+            const int lh = last / K, lg = last % K;
+            if (H == 1 || lh == hf) {  // this wavefront's node: its group holds the configuration
+                const int src = (lg << 3) + r;
+                cx = shfl_d(sx, src);
+                cy = shfl_d(sy, src);
+                cry = shfl_d(sry, src);
+            } else if constexpr (H > 1) {  // the other half's: the path's proposals again
+                bool mv2 = false;
+                apply(cx, cy, cry, mv2, steps, [&](int i) __attribute__((always_inline)) {
+                    return ((acc_steps >> i) & 1u) != 0;
+                });
+            }
+            const double* sl = streams_of(lh).ptr() + lg * S_W0;
             if (r < n) cph = (float)(-sl[S_FP + r]);
             if (r < nr) {
                 rpw0 = -sl[S_PW + r];
@@ -891,13 +926,13 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
                 rang1 = -sl[S_ANG + r + GL];
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last << 3);
+            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last);
             accepted += (unsigned int)nacc;
             // An accepted swap also exchanges z, rotX and rotZ (:675-700), object 1's values
             // through float temporaries, in step order (a later swap sees an earlier one's).
             for (int d = 0; d < steps; ++d) {
                 if (!((acc_steps >> d) & 1u)) continue;
-                const int qc = rec(cons + (unsigned int)d).code;
+                const int qc = __builtin_amdgcn_readlane(r_code, d);
                 const int q1 = rec_k1(qc), q2 = rec_k2(qc);
                 if (rec_mode(qc) == 2 && q1 >= 0) {
                     const int ia = gbase + q1, ib = gbase + q2;
@@ -916,7 +951,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
             }
         }
 #if MH_SPEC_DEBUG
-        if (chain == 0 && lane == 0) {  // [done, kb, cons, prod_seen, last, steps, cur0, nacc]
+        if (chain == 0 && lead && lane == 0) {  // [done, kb, cons, prod_seen, last, steps, cur0, nacc]
             const unsigned int base = g_spec_dbg_n;
             if (base + 8 < (1u << 16)) {
                 g_spec_dbg[base + 0] = (unsigned)done;
@@ -941,7 +976,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         }
         cons += (unsigned int)steps;
         done += steps;
-        if (lane == 0) CONS.put(0, cons);  // (wave 1 reads it between the next two barriers)
+        if (lead && lane == 0) CONS.put(0, cons);  // (wave 1 reads it between the next two barriers)
         SSTAMP(7);
 #if MH_STAMPS
         cyc[14] += 1;
@@ -949,11 +984,11 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
 #endif
     }
 #if MH_STAMPS
-    if (lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
+    if (lead && lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
         for (int k = 0; k < 16; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
 #endif
 
-    if (lane < n) {
+    if (lead && lane < n) {
         st[F_X * n + r] = cx;
         st[F_Y * n + r] = cy;
         st[F_RY * n + r] = cry;
@@ -961,7 +996,7 @@ __global__ void __launch_bounds__(64 * kSpecWaves) mh_spec_kernel(LaunchArgs a) 
         st[F_RX * n + r] = crx;
         st[F_RZ * n + r] = crz;
     }
-    if (lane == 0) {
+    if (lead && lane == 0) {
         ChainMeta m = m0;
         m.accepted = m0.accepted + accepted;
         m.draws = end_pos;
@@ -999,28 +1034,33 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsig
 }
 #endif
 
-size_t spec_lds_bytes(int /*waves_per_wg: always the chain's two*/) { return (size_t)kSpecBytes; }
+// The kernel instance: H = 2 (16 nodes, four wavefronts per chain) or 1 (8 nodes, two).
+size_t spec_lds_bytes(int halves) { return (size_t)(halves >= 2 ? spec_bytes<2>() : spec_bytes<1>()); }
 
-// Chains per workgroup (one: its two wavefronts share the chain), and wavefronts per chain.
+// Chains per workgroup (one: its wavefronts share the chain), and wavefronts per chain.
 int spec_waves() { return 1; }
-int spec_waves_per_chain() { return kSplit; }
+int spec_waves_per_chain(int halves) { return 2 * (halves >= 2 ? 2 : 1); }
 
 // Whether the speculative kernel serves a room: at most GL objects, RMAX relationships.
 bool spec_fits(int n, int c, int r) { return n >= 1 && n <= GL && c <= GL && r <= RMAX; }
 
-int spec_blocks_per_cu() {
+int spec_blocks_per_cu(int halves) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel, 64 * kSpecWaves,
-                                                     spec_lds_bytes(kSpecWaves)) != hipSuccess)
-        return 0;
-    return blocks;
+    const hipError_t e =
+        halves >= 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel<2>, 256,
+                                                                   spec_lds_bytes(2))
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel<1>, 128,
+                                                                   spec_lds_bytes(1));
+    return e == hipSuccess ? blocks : 0;
 }
 
-hipError_t launch_spec(const LaunchArgs& a, hipStream_t s) {
+hipError_t launch_spec(const LaunchArgs& a, int halves, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
-    const int64_t blocks = a.n_chains;  // one chain per workgroup
-    hipLaunchKernelGGL(mh_spec_kernel, dim3((unsigned)blocks), dim3(64 * kSpecWaves),
-                       spec_lds_bytes(kSpecWaves), s, a);
+    const dim3 grid((unsigned)a.n_chains);  // one chain per workgroup
+    if (halves >= 2)
+        hipLaunchKernelGGL(mh_spec_kernel<2>, grid, dim3(256), spec_lds_bytes(2), s, a);
+    else
+        hipLaunchKernelGGL(mh_spec_kernel<1>, grid, dim3(128), spec_lds_bytes(1), s, a);
     return hipGetLastError();
 }
 

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 REV=$1; NAME=$2
 T=$(mktemp -d)
-mkdir -p $T/metropolis-hastings-gpgpu_amd/csrc $T/include ablate
+mkdir -p $T/metropolis-hastings-gpgpu_amd/csrc $T/include abvar
 for f in $(git ls-tree --name-only $REV metropolis-hastings-gpgpu_amd/csrc/) include/mh_kernel.h; do
   git show $REV:$f > $T/$f
 done
