@@ -694,8 +694,9 @@ void prefault(void* p, size_t bytes) {
             return;
         }
     }
-    for (uintptr_t a = b; a < e; a = (a & ~(pg - 1)) + pg) *reinterpret_cast<volatile unsigned char*>(a) = 0;
-    static_cast<volatile unsigned char*>(p)[bytes - 1] = 0;
+    volatile unsigned char* c = static_cast<volatile unsigned char*>(p);
+    for (uintptr_t a = b; a < e; a = (a & ~(pg - 1)) + pg) c[a - b] = 0;  // one write per page
+    c[bytes - 1] = 0;
 }
 
 // The session's pinned staging chunks, at least min(bytes, kStageChunk) each.
