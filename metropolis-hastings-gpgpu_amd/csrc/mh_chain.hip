@@ -42,7 +42,7 @@ static __device__ unsigned long long g_phase_cycles[16];  // (XORWOW kernels: no
 __device__ unsigned long long g_phase_cycles[16];
 #endif
 #define MH_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
-#define MH_PHASE(ch, k, t0) do { unsigned long long _t; MH_STAMP(_t); (ch).aux->cyc[k] += _t - (t0); (t0) = _t; } while (0)
+#define MH_PHASE(ch, k, t0) do { unsigned long long _t; MH_STAMP(_t); stage((ch).aux)->cyc[k] += _t - (t0); (t0) = _t; } while (0)
 #else
 #define MH_STAMP(t) do { } while (0)
 #define MH_PHASE(ch, k, t0) do { } while (0)
@@ -105,6 +105,8 @@ __device__ __forceinline__ double pose_ry_var(const OwnPose<NPL>& op, int j, int
     return out;
 }
 
+// The chain's LDS. Every array that one lane writes and other lanes read is a Published view
+// (mh_common.h): lanes write through stage(ch.X), and each phase ends in hand_off(ch.X, ...).
 struct ChainPtrs {
     const RectShape* objs;  // room tables, staged once per workgroup into LDS (ChainLds)
     const RectShape* clrs;
@@ -112,19 +114,19 @@ struct ChainPtrs {
     const uint2* rix;  // [R] relationship i's objects {s | t << 16, as | at << 16}
     const float4* re0;  // [R] fp32 constants of the relationships' estimates (rel_est_consts)
     const float4* re1;
-    ObjP* P;
-    double *PX, *PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
-    double *CPHF, *RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
-    double* LCL;      // compacted non-zero Clearance terms (float values), capacity 2L
-    double* LPW;      // compacted non-zero PairWise / Angle terms, capacity lst_r each
-    double* LANG;
+    Published<ObjP> P;
+    Published<double> PX, PY;  // [N4] per-object double terms of the dense ordered sums (zero past N)
+    Published<double> CPHF, RMXF;  // [N4] per-object float terms (-cos phi, -row max), widened
+    Published<double> LCL;  // compacted non-zero Clearance terms (float values), capacity 2L
+    Published<double> LPW;  // compacted non-zero PairWise / Angle terms, capacity lst_r each
+    Published<double> LANG;
     int lst_r;
     double* zrr;      // HBM: this chain's z, rotX, rotZ rows (F_Z, F_RX, F_RZ of the pose block)
-    float4* OFF;
-    float4* CLA;
-    uint64_t* NZ;     // [2][C] row words of the non-zero Clearance pairs
-    int* PRE;         // [C] row prefix counts
-    ChainAux* aux;
+    Published<float4> OFF;
+    Published<float4> CLA;
+    Published<uint64_t> NZ;  // [2][C] row words of the non-zero Clearance pairs
+    Published<int> PRE;      // [C] row prefix counts
+    Published<ChainAux> aux;  // (the writer lane's record)
     const DevRoom* rm;  // LDS copy of the room scalars
     const double* zero4;  // four zero doubles (a finished replay lane reads these)
 };
@@ -137,37 +139,38 @@ struct ChainPtrs {
 // folded into its owner's accumulator (only for pathologically overlapping rooms).
 
 template <typename T>
-__device__ __forceinline__ void list_flush(const T* buf, int& cnt, double& acc, bool owner,
+__device__ __forceinline__ void list_flush(const Staged<T>& buf, int& cnt, double& acc, bool owner,
                                            bool to_float) {
-    wave_sync();
+    const Published<T> v = publish(buf);  // (every lane's appends)
     if (owner) {
         for (int l = 0; l < cnt; ++l) {
-            const double t = acc + (double)buf[l];
+            const double t = acc + (double)v[l];
             acc = to_float ? (double)(float)t : t;
         }
     }
     cnt = 0;
-    wave_sync();
+    (void)restage(v);  // (the owner's reads are done before any lane appends again)
 }
 
 // Appends, in lane order, the value of every lane whose `nz` is set (folding the list into its
 // owner's accumulator first only if these values would not fit).
 template <int L, typename T>
-__device__ __forceinline__ void list_append(T* buf, int cap, int& cnt, double& acc, bool owner,
-                                            bool to_float, T v, bool nz, int r, int gbase) {
+__device__ __forceinline__ void list_append(const Staged<T>& buf, int cap, int& cnt, double& acc,
+                                            bool owner, bool to_float, T v, bool nz, int r,
+                                            int gbase) {
     const uint64_t b = group_ballot<L>(nz, gbase);
     const int add = __builtin_popcountll(b);
     if (add == 0) return;
     if (cnt + add > cap) list_flush(buf, cnt, acc, owner, to_float);
-    if (nz) buf[cnt + __builtin_popcountll(b & ((1ull << r) - 1ull))] = v;
+    if (nz) buf.put(cnt + __builtin_popcountll(b & ((1ull << r) - 1ull)), v);
     cnt += add;
 }
 
 // Appends K values per lane in order k = 0..K-1 (each in lane order): one overflow test and
 // one count update for the batch.
 template <int L, int K, typename T>
-__device__ __forceinline__ void list_append_n(T* buf, int cap, int& cnt, double& acc, bool owner,
-                                              bool to_float, const T (&v)[K],
+__device__ __forceinline__ void list_append_n(const Staged<T>& buf, int cap, int& cnt, double& acc,
+                                              bool owner, bool to_float, const T (&v)[K],
                                               const bool (&nz)[K], int r, int gbase) {
     uint64_t b[K];
     int add = 0;
@@ -182,7 +185,7 @@ __device__ __forceinline__ void list_append_n(T* buf, int cap, int& cnt, double&
     int pos = cnt;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        if (nz[k]) buf[pos + __builtin_popcountll(b[k] & below)] = v[k];
+        if (nz[k]) buf.put(pos + __builtin_popcountll(b[k] & below), v[k]);
         pos += __builtin_popcountll(b[k]);
     }
     cnt = pos;
@@ -190,7 +193,7 @@ __device__ __forceinline__ void list_append_n(T* buf, int cap, int& cnt, double&
 
 // PairWiseCosts (:210-233) and PairWiseAngleCosts (:236-263) terms of relationship q (mh_common.h).
 __device__ __forceinline__ void rel_terms(const ChainPtrs& ch, int q, double& tpw, double& tang) {
-    rel_terms(ch.relc[q], ch.P, tpw, tang);
+    rel_terms(ch.relc[q], ch.P.ptr(), tpw, tang);
 }
 
 // ---- FocalPoint and relationship terms of one lane, exact or estimated ------------------------
@@ -207,7 +210,7 @@ __device__ __forceinline__ void exact_terms(const ChainPtrs& ch, const DevRoom& 
     const double fy = (double)(rm.fyf - p.yf), fx = (double)(rm.fxf - p.xf);
     double dy = fy, dx = fx, tpw = 0.0;
     float ti = 0.0f;
-    if (rel) tpw = rel_pair(ch.relc[i], ch.P, dy, dx, ti);
+    if (rel) tpw = rel_pair(ch.relc[i], ch.P.ptr(), dy, dx, ti);
     double a1 = 0.0, a2 = 0.0;
     if (rel || obj) a1 = atan2_ool(dy, dx);
     if (rel && obj) a2 = atan2_ool(fy, fx);
@@ -312,8 +315,8 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
                                              int r, int gbase, float4 boxj, const ClPairs& clp,
                                              ClPairs& clo, bool& colchg) {
     const int j = r;
-    const uint64_t* NZc = ch.NZ + clp.buf * c;
-    uint64_t* NZn = ch.NZ + (clp.buf ^ 1) * c;
+    const uint64_t* NZc = ch.NZ.ptr() + clp.buf * c;
+    const Staged<uint64_t> NZn = stage(ch.NZ.at((clp.buf ^ 1) * c));
     uint64_t cm = clp.cm;
     uint64_t w = (r < c) ? NZc[r] : 0ull;  // lane r's clearance row, patched below
     const int kk2[2] = {ka, kb};
@@ -340,13 +343,13 @@ __device__ __forceinline__ int inc_cl_update(const ChainPtrs& ch, int n, int c, 
         cm = (cm & ~(1ull << i)) | ((uint64_t)nzi << i);
         if (r == i) w = row;
     }
-    if (r < c) NZn[r] = w;
+    if (r < c) NZn.put(r, w);
     int total;
     const int pre = group_excl_scan<L>(r < c ? __builtin_popcountll(w) : 0, r, total);
-    if (r < c) ch.PRE[r] = pre;
+    if (r < c) stage(ch.PRE).put(r, pre);
     clo.cm = cm;
     clo.buf = clp.buf ^ 1;
-    wave_sync();
+    hand_off(ch.NZ, ch.PRE);  // the proposed rows and their prefix counts: the list build's
     return total;
 }
 
@@ -383,7 +386,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                            float out[8], SymRows<NPL>& sym, const SymRows<NPL>& prev, int ka,
                            int kb, ClPairs& clo, const ClPairs& clp, float u_acc = 0.0f,
                            CostIv cur = CostIv{0.0f, 0.0f}, int* fast = nullptr,
-                           CostIv* star_iv = nullptr, float* save = nullptr) {
+                           CostIv* star_iv = nullptr, bool save = false) {
     // The room scalars are read from the workgroup's LDS copy where they are used, not kept
     // live in SGPRs from the kernel arguments (that spilled ~140 SGPRs into VGPR lanes).
     // (the few-chains instance reads them from the kernel arguments: no LDS round trip on its
@@ -467,8 +470,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             // (to the replay's LDS streams at once: held in registers to the replay, the
             // doubles spilled on the exact paths)
             const double vx = (double)area * x, vy = (double)area * y;
-            ch.PX[i] = vx;
-            ch.PY[i] = vy;
+            stage(ch.PX).put(i, vx);
+            stage(ch.PY).put(i, vy);
             px[m] = (float)vx;
             py[m] = (float)vy;
             // FocalPointCosts term, Kernel.cu:271,277 with phi() of :185-188 (steps with one
@@ -490,7 +493,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             rrs[m] = rr;
             // Off-limits box at the object's pose; SurfaceAreaCosts terms, Kernel.cu:469-480.
             const float4 box = shape_box(os, p.xf, p.yf);
-            if constexpr (WITH_OL) ch.OFF[i] = box;
+            if constexpr (WITH_OL) stage(ch.OFF).put(i, box);
             sao[m] = comp_overlaps(rm, box);
             boxo[m] = box;
         }
@@ -509,7 +512,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         if (i < c) {
             const RectShape cs = ch.clrs[i];
             const ObjP ps = ch.P[cs.pad];
-            ch.CLA[i] = shape_box(cs, ps.xf, ps.yf);             // ClearanceCosts, :414-415
+            stage(ch.CLA).put(i, shape_box(cs, ps.xf, ps.yf));  // ClearanceCosts, :414-415
         }
         // SurfaceArea quirk: clearance i at object i's pose (cfg[i], :456). Steps with one
         // object per lane keep the overlaps unless object i moved, so most steps skip the pass.
@@ -525,7 +528,9 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         if constexpr (NPL == 1) clo.sac = sac[0];
     }
     }
-    wave_sync();
+    // Phase A's per-object terms and boxes: the Clearance pairs, OffLimits and the replay read
+    // other lanes'.
+    hand_off(ch.PX, ch.PY, ch.CLA, ch.OFF);
 
     // Phase B: symmetry rows, Kernel.cu:301-312. Row max over j of the reference's value,
     // which needs two correctly rounded square roots and ~25 fp64 operations per pair.
@@ -991,8 +996,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     for (int m = 0; m < NPL; ++m) {
         const int i = m * L + r;
         if (i < n) {
-            ch.CPHF[i] = -cph[m];
-            ch.RMXF[i] = -sym.mx[m];
+            stage(ch.CPHF).put(i, -cph[m]);
+            stage(ch.RMXF).put(i, -sym.mx[m]);
         }
     }
     // SurfaceAreaCosts: clearances (quirk box at cfg[i]) first, then objects (:453-480);
@@ -1020,7 +1025,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         const int j = r;
         const float4 boxj = boxo[0];
         if constexpr (INC_CL) {
-            const uint64_t* NZn = ch.NZ + clo.buf * c;
+            const uint64_t* NZn = ch.NZ.ptr() + clo.buf * c;
             if (cl_total <= 2 * L) {  // fits the list: write every term at its position
                 const uint64_t below = (1ull << j) - 1ull;
                 uint64_t bits = j < n ? clo.cm : 0ull;
@@ -1029,7 +1034,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                     bits &= bits - 1;
                     const int pos = ch.PRE[i] + __builtin_popcountll(NZn[i] & below);
                     if (MH_CK(i < c && pos >= 0 && pos < 2 * L, 6, i, pos))
-                        ch.LCL[pos] = (double)-overlap(ch.CLA[i], boxj);
+                        stage(ch.LCL).put(pos, (double)-overlap(ch.CLA[i], boxj));
                 }
                 cnt_cl = cl_total;
                 cl_done = true;
@@ -1044,7 +1049,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
                 const uint64_t row = group_ballot<L>(nzi, gbase);
                 cm |= (uint64_t)nzi << i;
                 if (nzi) clc += ov;
-                if (r == 0) ch.NZ[i] = row;
+                if (r == 0) stage(ch.NZ).put(i, row);
             }
             clo.cm = cm;
             clo.buf = 0;
@@ -1088,8 +1093,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             v[NPL + m] = (double)-a1;
             nz[NPL + m] = a1 != 0.0f;
         }
-        list_append_n<L, 2 * NPL, double>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, v, nz, r,
-                                          gbase);
+        list_append_n<L, 2 * NPL, double>(stage(ch.LCL), 2 * L, cnt_cl, acc, r == 4, true, v, nz,
+                                          r, gbase);
     }
     for (; ci < cend; ++ci) {
         const float4 A = A0n;  // box ci; box ci + 1 is in flight during the appends
@@ -1098,7 +1103,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         for (int m = 0; m < NPL; ++m) {
             const int j = m * L + r;
             const float ar = (j < n) ? overlap(A, offb[m]) : 0.0f;
-            list_append<L, double>(ch.LCL, 2 * L, cnt_cl, acc, r == 4, true, (double)-ar,
+            list_append<L, double>(stage(ch.LCL), 2 * L, cnt_cl, acc, r == 4, true, (double)-ar,
                                    ar != 0.0f, r, gbase);
         }
     }
@@ -1113,18 +1118,18 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
         if (m * L >= rm.r) break;
-        list_append<L, double>(ch.LPW, ch.lst_r, cnt_pw, acc, r == 6, false, -rpw[m],
+        list_append<L, double>(stage(ch.LPW), ch.lst_r, cnt_pw, acc, r == 6, false, -rpw[m],
                                rpw[m] != 0.0, r, gbase);
-        list_append<L, double>(ch.LANG, ch.lst_r, cnt_ang, acc, r == 7, false, -rang[m],
+        list_append<L, double>(stage(ch.LANG), ch.lst_r, cnt_ang, acc, r == 7, false, -rang[m],
                                rang[m] != 0.0, r, gbase);
     }
     for (int qb = NPL * L; qb < ((MH_ABLATE & 16) ? 0 : rm.r); qb += L) {  // R > L * NPL
         const int q = qb + r;
         double tpw = 0.0, tang = 0.0;
         if (q < rm.r) rel_terms(ch, q, tpw, tang);
-        list_append<L, double>(ch.LPW, ch.lst_r, cnt_pw, acc, r == 6, false, -tpw, tpw != 0.0,
-                               r, gbase);
-        list_append<L, double>(ch.LANG, ch.lst_r, cnt_ang, acc, r == 7, false, -tang,
+        list_append<L, double>(stage(ch.LPW), ch.lst_r, cnt_pw, acc, r == 6, false, -tpw,
+                               tpw != 0.0, r, gbase);
+        list_append<L, double>(stage(ch.LANG), ch.lst_r, cnt_ang, acc, r == 7, false, -tang,
                                tang != 0.0, r, gbase);
     }
     }
@@ -1135,10 +1140,11 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     // 6/7: PairWise / Angle lists (double, double). Every sequence is zero-padded to a multiple
     // of four terms; a lane reads four at a time (two ds_read_b128 of doubles or one of
     // floats) and keeps both a double- and a float-rounded walk of the same terms.
-    for (int q = cnt_cl + r; q < ((cnt_cl + 3) & ~3); q += L) ch.LCL[q] = 0.0;
-    for (int q = cnt_pw + r; q < ((cnt_pw + 3) & ~3); q += L) ch.LPW[q] = 0.0;
-    for (int q = cnt_ang + r; q < ((cnt_ang + 3) & ~3); q += L) ch.LANG[q] = 0.0;
-    wave_sync();
+    for (int q = cnt_cl + r; q < ((cnt_cl + 3) & ~3); q += L) stage(ch.LCL).put(q, 0.0);
+    for (int q = cnt_pw + r; q < ((cnt_pw + 3) & ~3); q += L) stage(ch.LPW).put(q, 0.0);
+    for (int q = cnt_ang + r; q < ((cnt_ang + 3) & ~3); q += L) stage(ch.LANG).put(q, 0.0);
+    // the replay's streams, as their lanes walk them
+    hand_off(ch.CPHF, ch.RMXF, ch.LCL, ch.LPW, ch.LANG);
     const double acc0 = acc;
     for (int rep = 0; rep < MH_REPS(32); ++rep) {
         MH_CLOBBER();
@@ -1146,16 +1152,16 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
         const double* dsrc = ch.zero4;
         int len = 0;
         if (k == 0 || k == 1) {
-            dsrc = k == 0 ? ch.PX : ch.PY;
+            dsrc = k == 0 ? ch.PX.ptr() : ch.PY.ptr();
             len = n;
         } else if (k == 2 || k == 3) {
-            dsrc = k == 2 ? ch.CPHF : ch.RMXF;
+            dsrc = k == 2 ? ch.CPHF.ptr() : ch.RMXF.ptr();
             len = n;
         } else if (k == 4) {
-            dsrc = ch.LCL;
+            dsrc = ch.LCL.ptr();
             len = cnt_cl;
         } else if (k == 6 || k == 7) {
-            dsrc = k == 6 ? ch.LPW : ch.LANG;
+            dsrc = k == 6 ? ch.LPW.ptr() : ch.LANG.ptr();
             len = k == 6 ? cnt_pw : cnt_ang;
         }
         len = (len + 3) & ~3;
@@ -1197,7 +1203,8 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     const float cl = (float)grp_get<L>(acc, 4, gbase);
     const double pw = grp_get<L>(acc, 6, gbase);
     const double ang = grp_get<L>(acc, 7, gbase);
-    wave_sync();
+    // (the replay's reads are done before a lane rewrites its streams)
+    hand_off(ch.PX, ch.PY, ch.CPHF, ch.RMXF, ch.LCL, ch.LPW, ch.LANG);
     const float vb = (float)(-1.0 * distance_f(nx / rm.denom, ny / rm.denom, rm.cxf, rm.cyf));
 
     if (r == 0) MH_PHASE(ch, 6, t0);
@@ -1230,7 +1237,7 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
     t = t + out[7];
     out[0] = t;
     if (save && r == 0)  // (the caller then keeps only the total in a register)
-        for (int k = 0; k < 8; ++k) save[k] = out[k];
+        for (int k = 0; k < 8; ++k) stage(ch.aux)->star[k] = out[k];
 }
 
 // ---- propose(), Kernel.cu:566-704, applied in place --------------------------------------
@@ -1267,7 +1274,7 @@ __device__ __forceinline__ void write_obj(const ChainPtrs& ch, OwnPose<NPL>& op,
         p.yf = (float)y;
         p.rotYf = (float)ry;
         p.pad = 0.0f;
-        ch.P[k] = p;
+        stage(ch.P).put(k, p);
     }
 }
 
@@ -1294,9 +1301,10 @@ __device__ MH_EVAL_ATTR int2 propose(Rng& rng, const DevRoom& rm, const unsigned
         else if (y + (double)dy < rm.rmin_y) y = rm.rmin_y;
         else y = y + (double)dy;
         if (writer) {
-            ch.aux->b[0] = b0;
-            ch.aux->nb = 1;
-            ch.aux->swap_a = -1;
+            const Staged<ChainAux> ax = stage(ch.aux);
+            ax->b[0] = b0;
+            ax->nb = 1;
+            ax->swap_a = -1;
         }
         write_obj<L, NPL>(ch, op, r, writer, k, x, y, b0.ry);
         return make_int2(k, -1);
@@ -1310,9 +1318,10 @@ __device__ MH_EVAL_ATTR int2 propose(Rng& rng, const DevRoom& rm, const unsigned
         if (ry < 0) ry = ry + kTwoPI;
         else if (ry > kTwoPI) ry = ry - kTwoPI;
         if (writer) {
-            ch.aux->b[0] = b0;
-            ch.aux->nb = 1;
-            ch.aux->swap_a = -1;
+            const Staged<ChainAux> ax = stage(ch.aux);
+            ax->b[0] = b0;
+            ax->nb = 1;
+            ax->swap_a = -1;
         }
         write_obj<L, NPL>(ch, op, r, writer, k, b0.x, b0.y, ry);
         return make_int2(k, -1);
@@ -1320,8 +1329,9 @@ __device__ MH_EVAL_ATTR int2 propose(Rng& rng, const DevRoom& rm, const unsigned
     // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
     if (n < 2) {
         if (writer) {
-            ch.aux->nb = 0;
-            ch.aux->swap_a = -1;
+            const Staged<ChainAux> ax = stage(ch.aux);
+            ax->nb = 0;
+            ax->swap_a = -1;
         }
         return make_int2(-1, -1);
     }
@@ -1330,11 +1340,12 @@ __device__ MH_EVAL_ATTR int2 propose(Rng& rng, const DevRoom& rm, const unsigned
     const Backup b0 = read_obj<L, NPL>(op, ka, gbase);
     const Backup b1 = read_obj<L, NPL>(op, kb, gbase);
     if (writer) {
-        ch.aux->b[0] = b0;
-        ch.aux->b[1] = b1;
-        ch.aux->nb = 2;
-        ch.aux->swap_a = ka;
-        ch.aux->swap_b = kb;
+        const Staged<ChainAux> ax = stage(ch.aux);
+        ax->b[0] = b0;
+        ax->b[1] = b1;
+        ax->nb = 2;
+        ax->swap_a = ka;
+        ax->swap_b = kb;
     }
     write_obj<L, NPL>(ch, op, r, writer, ka, b1.x, b1.y, b1.ry);
     write_obj<L, NPL>(ch, op, r, writer, kb, (double)(float)b0.x, (double)(float)b0.y,
@@ -1503,35 +1514,35 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     ch.rix = rix_l;
     ch.re0 = re0_l;
     ch.re1 = re1_l;
-    ch.P = reinterpret_cast<ObjP*>(base + F.P);
-    ch.PX = reinterpret_cast<double*>(base + F.PX);
-    ch.PY = reinterpret_cast<double*>(base + F.PY);
-    ch.CPHF = reinterpret_cast<double*>(base + F.CPHF);
-    ch.RMXF = reinterpret_cast<double*>(base + F.RMXF);
-    ch.LCL = reinterpret_cast<double*>(base + F.LCL);
-    ch.LPW = reinterpret_cast<double*>(base + a.lay.LPW);
+    ch.P = {reinterpret_cast<ObjP*>(base + F.P)};
+    ch.PX = {reinterpret_cast<double*>(base + F.PX)};
+    ch.PY = {reinterpret_cast<double*>(base + F.PY)};
+    ch.CPHF = {reinterpret_cast<double*>(base + F.CPHF)};
+    ch.RMXF = {reinterpret_cast<double*>(base + F.RMXF)};
+    ch.LCL = {reinterpret_cast<double*>(base + F.LCL)};
+    ch.LPW = {reinterpret_cast<double*>(base + a.lay.LPW)};
     ch.lst_r = a.lay.lst_r;
-    ch.LANG = reinterpret_cast<double*>(base + a.lay.LANG);
+    ch.LANG = {reinterpret_cast<double*>(base + a.lay.LANG)};
     ch.zrr = a.st + chain * (int64_t)(F_COUNT * n) + F_Z * n;
-    ch.OFF = reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0));
+    ch.OFF = {reinterpret_cast<float4*>(base + (a.lay.OFF >= 0 ? a.lay.OFF : 0))};
     {
         constexpr int kCla = fixed_cla(F);
         const int c1 = a.rm.c > 0 ? a.rm.c : 1;
         MH_CK(a.lay.CLA == kCla && a.lay.NZ == kCla + 16 * c1, 13, a.lay.CLA, kCla);
-        ch.CLA = reinterpret_cast<float4*>(base + kCla);
-        ch.NZ = reinterpret_cast<uint64_t*>(base + kCla + 16 * c1);
-        ch.PRE = reinterpret_cast<int*>(base + kCla + 32 * c1);
+        ch.CLA = {reinterpret_cast<float4*>(base + kCla)};
+        ch.NZ = {reinterpret_cast<uint64_t*>(base + kCla + 16 * c1)};
+        ch.PRE = {reinterpret_cast<int*>(base + kCla + 32 * c1)};
     }
-    ch.aux = reinterpret_cast<ChainAux*>(base + F.AUX);
+    ch.aux = {reinterpret_cast<ChainAux*>(base + F.AUX)};
     ch.rm = rm_l;
     ch.zero4 = reinterpret_cast<const double*>(lds + F.h_zero);
 
     // Zero the dense replay streams past N (never written afterwards).
     for (int i = n + r; i < a.lay.N4; i += L) {
-        ch.PX[i] = 0.0;
-        ch.PY[i] = 0.0;
-        ch.CPHF[i] = 0.0;
-        ch.RMXF[i] = 0.0;
+        stage(ch.PX).put(i, 0.0);
+        stage(ch.PY).put(i, 0.0);
+        stage(ch.CPHF).put(i, 0.0);
+        stage(ch.RMXF).put(i, 0.0);
     }
     // Stage the configuration: double poses into this lane's registers, float pose words
     // into LDS.
@@ -1560,10 +1571,11 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             p.yf = (float)y;
             p.rotYf = (float)ry;
             p.pad = 0.0f;
-            ch.P[i] = p;
+            stage(ch.P).put(i, p);
         }
     }
-    wave_sync();
+    // the staged configuration and the replay streams' zero tails
+    hand_off(ch.P, ch.PX, ch.PY, ch.CPHF, ch.RMXF);
 
     float cur[8];
     SymRows<NPL> sym;  // symmetry row maxima of the current configuration
@@ -1585,7 +1597,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         const ChainMeta m0 = a.meta[chain];
         const bool writer = (r == 0);
         if (writer)
-            for (int k = 0; k < 8; ++k) ch.aux->cur[k] = m0.costs[k];
+            for (int k = 0; k < 8; ++k) stage(ch.aux)->cur[k] = m0.costs[k];
         float cur_total = m0.costs[0];
         bool cur_exact = true;  // (plain steps: false after a proposal accepted on the bound)
         CostIv cur_iv{cur_total, cur_total};
@@ -1595,7 +1607,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         Rng rng;
         if constexpr (std::is_same<Rng, WaveRngLds>::value) {
             rng.bsl = reinterpret_cast<float*>(base + F.RNG);
-            rng.ss = ch.aux->rng_key;
+            rng.ss = stage(ch.aux)->rng_key;  // (WaveRngLds hands its key words off itself)
         }
         rng_load(rng, a, chain, m0);
         // This launch's accepted count (at most `iterations`); the meta record's count, rung and
@@ -1610,7 +1622,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
         eval_costs<L, NPL, false, false>(a, ch, op, r, gbase, cur, sym, sym, -1, -1, cl, cl);
 #if MH_STAMPS
         if (writer)
-            for (int k = 0; k < 12; ++k) ch.aux->cyc[k] = 0;
+            for (int k = 0; k < 12; ++k) stage(ch.aux)->cyc[k] = 0;
 #endif
 #pragma clang loop unroll(disable)
         for (int it = 0; it < a.iterations; ++it) {
@@ -1620,7 +1632,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             const int2 kk = propose<L, NPL>(rng, OP == OP_STEP_FEW ? a.rm : *rm_l, frozen, ch, op,
                                             r, gbase, writer);
             MH_CK(kk.x < n && kk.y < n && kk.x >= -1 && kk.y >= -1, 11, kk.x, kk.y);
-            wave_sync();
+            hand_off(ch.P, ch.aux);  // the proposal's pose words and its undo record
             if (writer) MH_PHASE(ch, 0, ts);
             float sc[8];
             SymRows<NPL> ss;
@@ -1637,7 +1649,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             if constexpr (FASTK) u_acc = rng.uniform();
             eval_costs<L, NPL, false, true, FASTK, OP == OP_STEP_FEW>(
                 a, ch, op, r, gbase, sc, ss, sym, kk.x, kk.y, cls, cl, u_acc, cur_iv, &fast,
-                &star_iv, ch.aux->star);
+                &star_iv, true);
             // (exact costs only; a scalar register where the chain owns the wavefront)
             const float star0 = fast != BOUND_OPEN ? 0.0f : L == 64 ? uniform_f(sc[0]) : sc[0];
             MH_STAMP(ts);
@@ -1704,16 +1716,17 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                     const Backup s0 = read_obj<L, NPL>(op, k0, gbase);
                     const Backup s1 = read_obj<L, NPL>(op, k1, gbase);
                     restore<L, NPL>(ch, op, r, writer, kk);
-                    wave_sync();
+                    hand_off(ch.P, ch.aux);  // the current configuration again
                     float cx[8];
                     SymRows<NPL> sx;
                     ClPairs clx;
                     eval_costs<L, NPL, false, true>(a, ch, op, r, gbase, cx, sx, ss, kk.x, kk.y, clx,
                                                     cls);
                     if (writer) {
-                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = cx[k];
-                        if (nb > 0) ch.aux->b[0] = s0;
-                        if (nb > 1) ch.aux->b[1] = s1;
+                        const Staged<ChainAux> ax = stage(ch.aux);
+                        for (int k = 0; k < 8; ++k) ax->cur[k] = cx[k];
+                        if (nb > 0) ax->b[0] = s0;
+                        if (nb > 1) ax->b[1] = s1;
                     }
 #if MH_STAMPS
                     if (writer) ch.aux->cyc[11] += 1;
@@ -1728,14 +1741,14 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                         atomicAdd(&g_decide[3], 1ull);
                     }
 #endif
-                    wave_sync();
+                    hand_off(ch.aux);  // its exact costs, and the proposal's poses as the undo record
                     if (u_acc < accept_threshold(kBeta * ((double)star0 - (double)cur_total))) {
                         restore<L, NPL>(ch, op, r, writer, kk);  // the proposal again
                         fast = BOUND_ACCEPT + 1;  // accepted with exact costs (below)
                     } else {
                         fast = BOUND_REJECT + 16;  // rejected, already undone
                     }
-                    wave_sync();
+                    hand_off(ch.P);
                 }
             }
             // Best-of-chain: star is judged before Accept, Kernel.cu:808-816.
@@ -1775,13 +1788,13 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                 }
                 if (writer) {
                     if (exact)
-                        for (int k = 0; k < 8; ++k) ch.aux->cur[k] = ch.aux->star[k];
+                        for (int k = 0; k < 8; ++k) stage(ch.aux)->cur[k] = ch.aux->star[k];
                     commit_swap_zrr(ch, n);
                 }
             } else if (fast != BOUND_REJECT + 16) {
                 restore<L, NPL>(ch, op, r, writer, kk);
             }
-            wave_sync();
+            hand_off(ch.P, ch.aux);  // the step's configuration and current costs
             if (writer) MH_PHASE(ch, 7, ts);
         }
         if (!cur_exact) {
@@ -1792,8 +1805,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
             ClPairs clx;
             eval_costs<L, NPL, false, true>(a, ch, op, r, gbase, cx, sx, sym, -1, -1, clx, cl);
             if (writer)
-                for (int k = 0; k < 8; ++k) ch.aux->cur[k] = cx[k];
-            wave_sync();
+                for (int k = 0; k < 8; ++k) stage(ch.aux)->cur[k] = cx[k];
+            hand_off(ch.aux);
         }
 #if MH_STAMPS
         if (writer)
@@ -1869,8 +1882,8 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
     }
     if constexpr (OP == OP_INIT) {
         if (a.track != TRACK_OFF) {  // cfgBest := cfgCurrent, Kernel.cu:779-782
-            if (r == 0) ch.aux->swap_a = -1;
-            wave_sync();
+            if (r == 0) stage(ch.aux)->swap_a = -1;
+            hand_off(ch.aux);
             save_best_pose<L, NPL>(ch, op, a.best + chain * (int64_t)(F_COUNT * n), n, r);
         }
     }

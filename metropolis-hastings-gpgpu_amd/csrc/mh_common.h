@@ -88,24 +88,41 @@ __device__ __forceinline__ void wave_sync() {
 // ---- cross-lane LDS hand-offs -------------------------------------------------------------
 // LDS that some lanes of a wavefront write and other lanes read changes hands in phases (round
 // 3 lost chains to a missing wave_sync after a one-lane store). Lanes write through a Staged<T>
-// view (put only); publish() -- which holds the wave_sync -- returns Published<T> views (reads
-// only) of the arrays it is given; restage() turns a published array back into a staged one
-// (also a wave_sync: every lane's reads are done before any lane rewrites). A cross-lane read
-// with no publish() between it and the writes does not compile. (The speculative kernel is
-// written this way; the older kernels keep explicit wave_sync() calls, checked by the parity
-// suite.)
+// view (put, or a record's fields through ->); a hand-off -- the only wave_sync outside this
+// header -- makes the writes every lane's and orders every earlier read before later writes:
+//  * publish(staged...) returns Published<T> views (reads only) of the arrays it is given, and
+//    restage(published...) hands them back for rewriting: the speculative kernel's locals;
+//  * the full-evaluation and incremental kernels keep their chain's arrays in ChainPtrs /
+//    DeltaPtrs as Published<T> members, so a plain assignment to one does not compile: a lane
+//    writes through stage(ch.X) and the phase ends in hand_off(ch.X, ...), which names the arrays
+//    changing hands there.
 template <class T>
 struct Published {
     const T* p;
     __device__ __forceinline__ const T& operator[](int i) const { return p[i]; }
     __device__ __forceinline__ const T* ptr() const { return p; }
+    __device__ __forceinline__ const T* operator->() const { return p; }
+    __device__ __forceinline__ Published<T> at(int off) const { return Published<T>{p + off}; }
 };
 template <class T>
 struct Staged {
     T* p;
     __device__ __forceinline__ void put(int i, const T& v) const { p[i] = v; }
     __device__ __forceinline__ Staged<T> at(int off) const { return Staged<T>{p + off}; }
+    __device__ __forceinline__ T* operator->() const { return p; }  // (a record's fields)
+    __device__ __forceinline__ T* ptr() const { return p; }
 };
+// This lane is about to write an array whose readers hold its Published view: its writes reach
+// other lanes at the next hand_off() naming the array (no synchronisation here).
+template <class T>
+__device__ __forceinline__ Staged<T> stage(const Published<T>& v) {
+    return Staged<T>{const_cast<T*>(v.p)};
+}
+// The hand-off of the arrays named: one wave_sync (the arguments document what changes hands).
+template <class... T>
+__device__ __forceinline__ void hand_off(const Published<T>&...) {
+    wave_sync();
+}
 // publish(a, ...): one wave_sync, then the arrays' read views (`auto [av, bv] = publish(a, b);`).
 template <class A, class B>
 struct Pub2 { Published<A> a; Published<B> b; };

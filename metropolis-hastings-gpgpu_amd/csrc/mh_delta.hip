@@ -118,17 +118,19 @@ struct DeltaPtrs {
     const float *AREA, *ONES;  // replay streams shared by the workgroup
     const double* ZERO;   // double[DL] zeros
     const float* ZEROF;   // 4 zero floats
-    double *X, *Y;
-    float4* BOX;  // object off-limits boxes at the current poses, zero past N
-    float* RYF;   // (float)rotY
-    float* CPH;   // -cos(phi): the FocalPoint terms (the replay's stream), zero past N
-    float* NMX;   // -(row max) of the proposed rows: the replay's Symmetry stream
-    float4* CLA;  // boxes of clearances 64.. (the first 64: registers, Own::cla0)
-    uint64_t* NZ;  // pair words of clearances 64.. (the first 64 rows: registers, Own::nz0)
-    uint32_t *SAM, *SAMB;
-    double *RPW, *RANG;
-    float *LCL, *LSA;
-    DeltaAux* aux;
+    // (every array that one lane writes and other lanes read is a Published view, mh_common.h:
+    // lanes write through stage(ch.X), and each phase ends in hand_off(ch.X, ...))
+    Published<double> X, Y;
+    Published<float4> BOX;  // object off-limits boxes at the current poses, zero past N
+    Published<float> RYF;   // (float)rotY
+    Published<float> CPH;   // -cos(phi): the FocalPoint terms (the replay's stream), zero past N
+    Published<float> NMX;   // -(row max) of the proposed rows: the replay's Symmetry stream
+    Published<float4> CLA;  // boxes of clearances 64.. (the first 64: registers, Own::cla0)
+    Published<uint64_t> NZ;  // pair words of clearances 64.. (the first 64 rows: registers, Own::nz0)
+    Published<uint32_t> SAM, SAMB;
+    Published<double> RPW, RANG;
+    Published<float> LCL, LSA;
+    Published<DeltaAux> aux;  // (the writer lane's record)
     double* zrr;  // HBM: z, rotX, rotZ rows of this chain
     int W, SW, cap_cl, cap_sa, NP, NR, DL;
 };
@@ -161,7 +163,7 @@ __device__ __forceinline__ float4 cla_get(const DeltaPtrs& ch, const Own<S>& o, 
 template <int S>
 __device__ __forceinline__ void cla_put(const DeltaPtrs& ch, Own<S>& o, int ci, float4 v) {
     if (ci < 64) o.cla0 = v;
-    else ch.CLA[ci - 64] = v;
+    else stage(ch.CLA).put(ci - 64, v);
 }
 
 // SurfaceAreaCosts entry e (Kernel.cu:453-480): clearance e's box at cfg[e] (the reference's
@@ -201,8 +203,8 @@ __device__ __forceinline__ bool wild_pose(double x, double y, double ry) {
 
 __device__ __forceinline__ void sam_put(const DeltaPtrs& ch, int e, bool nz) {
     const uint32_t bit = 1u << (e & 31);
-    if (nz) atomicOr(&ch.SAM[e >> 5], bit);
-    else atomicAnd(&ch.SAM[e >> 5], ~bit);
+    if (nz) atomicOr(stage(ch.SAM).ptr() + (e >> 5), bit);
+    else atomicAnd(stage(ch.SAM).ptr() + (e >> 5), ~bit);
 }
 
 // ---- symmetry rows ------------------------------------------------------------------------
@@ -373,7 +375,7 @@ __device__ __forceinline__ void nz_row(const DeltaPtrs& ch, Own<S>& o, int n, in
         if (ci < 64) {
             if (r == ci) o.nz0[w] = word;
         } else if (r == 0) {
-            ch.NZ[(ci - 64) * S + w] = word;
+            stage(ch.NZ).put((ci - 64) * S + w, word);
         }
     }
 }
@@ -397,7 +399,7 @@ __device__ __forceinline__ bool clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
         }
     }
     chg0 = (rows & 1ull) != 0;  // (a moved row is rebuilt below)
-    wave_sync();
+    hand_off(ch.CLA);  // the moved clearances' boxes (64 and up: LDS)
     // Columns ka, kb of the rows whose clearance did not move (lane-owned rows).
     for (int s2 = 0; s2 < 2; ++s2) {
         const int j = s2 == 0 ? ka : kb;
@@ -418,7 +420,7 @@ __device__ __forceinline__ bool clearance_delta(const DeltaPtrs& ch, Own<S>& o, 
 #pragma unroll
                 for (int q = 0; q < S; ++q) o.nz0[q] = q == wj ? w1 : o.nz0[q];
             } else {
-                uint64_t* wd = &ch.NZ[(ci - 64) * S + (j >> 6)];
+                uint64_t* wd = stage(ch.NZ).ptr() + (ci - 64) * S + (j >> 6);
                 *wd = nz ? (*wd | bit) : (*wd & ~bit);
             }
         }
@@ -516,8 +518,8 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
                 else est->eang[1] = ea;
             }
             if (amb) rel_terms_of(ch.relg[q], [&ch](int k) { return obj_pose(ch, k); }, tpw, tang);
-            ch.RPW[q] = -tpw;
-            ch.RANG[q] = -tang;
+            stage(ch.RPW).put(q, -tpw);
+            stage(ch.RANG).put(q, -tang);
         }
     }
 }
@@ -535,8 +537,8 @@ __device__ __forceinline__ void rels_undo(const DeltaPtrs& ch, int nr, int ka, i
         if (k < bk.cnt) {
             const int q = bk.slot[k] * L + r;
             const double p = ch.RPW[q], g = ch.RANG[q];
-            ch.RPW[q] = bk.pw[k];
-            ch.RANG[q] = bk.ang[k];
+            stage(ch.RPW).put(q, bk.pw[k]);
+            stage(ch.RANG).put(q, bk.ang[k]);
             bk.pw[k] = p;
             bk.ang[k] = g;
         }
@@ -611,7 +613,7 @@ __device__ __forceinline__ int build_cl_list(const DeltaPtrs& ch, const Own<S>& 
                     const float v = -overlap(A, obj_box(ch, j));
                     acc += v;
                     accp = fmaf((float)pos, -v, accp);
-                    if (pos >= lo && pos < lo + ch.cap_cl) ch.LCL[pos - lo] = v;
+                    if (pos >= lo && pos < lo + ch.cap_cl) stage(ch.LCL).put(pos - lo, v);
                     ++pos;
                 }
             }
@@ -650,7 +652,7 @@ __device__ __forceinline__ int build_sa_list(const DeltaPtrs& ch, int n, int c, 
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (tv[u] != 0.0f) {
-                    if (pos >= lo && pos < lo + ch.cap_sa) ch.LSA[pos - lo] = -tv[u];
+                    if (pos >= lo && pos < lo + ch.cap_sa) stage(ch.LSA).put(pos - lo, -tv[u]);
                     ++pos;
                 }
         }
@@ -728,10 +730,10 @@ template <int S>
 __device__ __forceinline__ void write_pose(const DeltaPtrs& ch, Own<S>& o, int r, bool writer,
                                            int k, double x, double y, double ry) {
     if (writer) {
-        ch.X[k] = x;
-        ch.Y[k] = y;
-        ch.BOX[k] = shape_box(ch.objs[k], (float)x, (float)y);
-        ch.RYF[k] = (float)ry;
+        stage(ch.X).put(k, x);
+        stage(ch.Y).put(k, y);
+        stage(ch.BOX).put(k, shape_box(ch.objs[k], (float)x, (float)y));
+        stage(ch.RYF).put(k, (float)ry);
     }
     const bool own = r == (k & 63);
     slot_put<S>(o.ry, k >> 6, ry, own);
@@ -759,9 +761,10 @@ __device__ __forceinline__ int2 propose(Rng& rng, const DevRoom& rm, const unsig
         else if (y + (double)dy < rm.rmin_y) y = rm.rmin_y;
         else y = y + (double)dy;
         if (writer) {
-            ch.aux->b[0] = b0;
-            ch.aux->nb = 1;
-            ch.aux->swap_a = -1;
+            const Staged<DeltaAux> ax = stage(ch.aux);
+            ax->b[0] = b0;
+            ax->nb = 1;
+            ax->swap_a = -1;
         }
         write_pose<S>(ch, o, r, writer, k, x, y, b0.ry);
         return make_int2(k, -1);
@@ -775,9 +778,10 @@ __device__ __forceinline__ int2 propose(Rng& rng, const DevRoom& rm, const unsig
         if (ry < 0) ry = ry + kTwoPI;
         else if (ry > kTwoPI) ry = ry - kTwoPI;
         if (writer) {
-            ch.aux->b[0] = b0;
-            ch.aux->nb = 1;
-            ch.aux->swap_a = -1;
+            const Staged<DeltaAux> ax = stage(ch.aux);
+            ax->b[0] = b0;
+            ax->nb = 1;
+            ax->swap_a = -1;
         }
         write_pose<S>(ch, o, r, writer, k, b0.x, b0.y, ry);
         return make_int2(k, -1);
@@ -785,8 +789,9 @@ __device__ __forceinline__ int2 propose(Rng& rng, const DevRoom& rm, const unsig
     // swap, Kernel.cu:655-703: object 1's pose travels through float temporaries.
     if (n < 2) {
         if (writer) {
-            ch.aux->nb = 0;
-            ch.aux->swap_a = -1;
+            const Staged<DeltaAux> ax = stage(ch.aux);
+            ax->nb = 0;
+            ax->swap_a = -1;
         }
         return make_int2(-1, -1);
     }
@@ -795,11 +800,12 @@ __device__ __forceinline__ int2 propose(Rng& rng, const DevRoom& rm, const unsig
     const DBackup b0 = read_obj<S>(ch, o, ka);
     const DBackup b1 = read_obj<S>(ch, o, kb);
     if (writer) {
-        ch.aux->b[0] = b0;
-        ch.aux->b[1] = b1;
-        ch.aux->nb = 2;
-        ch.aux->swap_a = ka;
-        ch.aux->swap_b = kb;
+        const Staged<DeltaAux> ax = stage(ch.aux);
+        ax->b[0] = b0;
+        ax->b[1] = b1;
+        ax->nb = 2;
+        ax->swap_a = ka;
+        ax->swap_b = kb;
     }
     write_pose<S>(ch, o, r, writer, ka, b1.x, b1.y, b1.ry);
     write_pose<S>(ch, o, r, writer, kb, (double)(float)b0.x, (double)(float)b0.y,
@@ -903,25 +909,25 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     int lim = ch.NP;  // this lane's stream length; past it the lane reads ones / zeros
     if (k < 2) {
         ms = ch.AREA;
-        ds = k == 0 ? ch.X : ch.Y;
+        ds = k == 0 ? ch.X.ptr() : ch.Y.ptr();
     } else if (k == 2) {
-        fs = ch.CPH;
+        fs = ch.CPH.ptr();
         fstream = true;
     } else if (k == 3) {
-        fs = ch.NMX;
+        fs = ch.NMX.ptr();
         fstream = true;
     } else if (k == 4) {
-        fs = ch.LCL;
+        fs = ch.LCL.ptr();
         fstream = true;
     } else if (k == 5) {
-        fs = ch.LSA;  // (its capacity may be below NP: the stream ends at the zero-filled end)
+        fs = ch.LSA.ptr();  // (its capacity may be below NP: the stream ends at the zero-filled end)
         fstream = true;
         lim = (min(cnt_sa, ch.cap_sa) + 3) & ~3;
     } else if (k == 6) {
-        ds = ch.RPW;
+        ds = ch.RPW.ptr();
         lim = ch.NR;
     } else if (k == 7) {
-        ds = ch.RANG;
+        ds = ch.RANG.ptr();
         lim = ch.NR;
     }
     double accf = 0.0, accd = 0.0;  // float- and double-accumulated walks of the same terms
@@ -960,20 +966,20 @@ __device__ __forceinline__ void replay(const DeltaPtrs& ch, const Own<S>& o, int
     const int walked = min(lim, ch.DL);  // what the dense walk covered of this lane's stream
     if (tail > walked) af = list_walk(fs, walked, tail, af);
     for (int lo = ch.cap_cl; lo < cnt_cl; lo += ch.cap_cl) {
-        wave_sync();
+        hand_off(ch.LCL);  // (the previous window's walk is done before the list is rebuilt)
         build_cl_list<S>(ch, o, rm.c, r, lo);
         const int m = min(ch.cap_cl, cnt_cl - lo);
-        for (int l = m + r; l < ((m + 3) & ~3); l += L) ch.LCL[l] = 0.0f;
-        wave_sync();
-        if (k == 4) af = list_walk(ch.LCL, 0, (m + 3) & ~3, af);
+        for (int l = m + r; l < ((m + 3) & ~3); l += L) stage(ch.LCL).put(l, 0.0f);
+        hand_off(ch.LCL);  // the window, to its walking lane
+        if (k == 4) af = list_walk(ch.LCL.ptr(), 0, (m + 3) & ~3, af);
     }
     for (int lo = ch.cap_sa; lo < cnt_sa; lo += ch.cap_sa) {
-        wave_sync();
+        hand_off(ch.LSA);
         build_sa_list(ch, n, rm.c, r, lo);
         const int m = min(ch.cap_sa, cnt_sa - lo);
-        for (int l = m + r; l < ((m + 3) & ~3); l += L) ch.LSA[l] = 0.0f;
-        wave_sync();
-        if (k == 5) af = list_walk(ch.LSA, 0, (m + 3) & ~3, af);
+        for (int l = m + r; l < ((m + 3) & ~3); l += L) stage(ch.LSA).put(l, 0.0f);
+        hand_off(ch.LSA);
+        if (k == 5) af = list_walk(ch.LSA.ptr(), 0, (m + 3) & ~3, af);
     }
     accf = (double)af;
     const bool acc_float = (k == 0 || k == 1 || k == 3 || k == 4 || k == 5);
@@ -1019,14 +1025,15 @@ __device__ __forceinline__ void replay_config(const DeltaPtrs& ch, const typenam
     // zero past each list's end: to NP for the dense walk, to round4 for the list walk
     const int zcl = max(ch.NP, (min(cnt_cl, ch.cap_cl) + 3) & ~3);
     const int zsa = (min(cnt_sa, ch.cap_sa) + 3) & ~3;  // (lane 5's dense stream ends there)
-    for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) ch.LCL[l] = 0.0f;
-    for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) ch.LSA[l] = 0.0f;
+    for (int l = min(cnt_cl, ch.cap_cl) + r; l < zcl; l += L) stage(ch.LCL).put(l, 0.0f);
+    for (int l = min(cnt_sa, ch.cap_sa) + r; l < zsa; l += L) stage(ch.LSA).put(l, 0.0f);
 #pragma unroll
     for (int t = 0; t < S; ++t) {
         const int i = t * L + r;
-        if (i < n) ch.NMX[i] = -mx[t];
+        if (i < n) stage(ch.NMX).put(i, -mx[t]);
     }
-    wave_sync();
+    // the replay's streams, as their lanes walk them
+    hand_off(ch.X, ch.Y, ch.CPH, ch.NMX, ch.LCL, ch.LSA, ch.RPW, ch.RANG);
     replay<S>(ch, o, n, cnt_cl, cnt_sa, r, out, dense);
 }
 
@@ -1044,7 +1051,7 @@ __device__ __forceinline__ void fix_estimates(const DeltaPtrs& ch, const Own<S>&
             const float w = focal_cos(*ch.rm, o.xf[t], o.yf[t], (float)o.ry[t]);
             MH_CK(fabsf(-ch.CPH[i] - w) <= kDeltaCph, 30, __float_as_uint(-ch.CPH[i]),
                   __float_as_uint(w));
-            ch.CPH[i] = -w;
+            stage(ch.CPH).put(i, -w);
         }
     }
 #pragma unroll
@@ -1058,12 +1065,12 @@ __device__ __forceinline__ void fix_estimates(const DeltaPtrs& ch, const Own<S>&
                   __float_as_uint((float)-ch.RPW[q]), __float_as_uint((float)tpw));
             MH_CK(fabs(-ch.RANG[q] - tang) <= (double)est.eang[u], 32,
                   __float_as_uint((float)-ch.RANG[q]), __float_as_uint((float)tang));
-            ch.RPW[q] = -tpw;
-            ch.RANG[q] = -tang;
+            stage(ch.RPW).put(q, -tpw);
+            stage(ch.RANG).put(q, -tang);
         }
     }
     est.obj = est.rel = 0u;
-    wave_sync();
+    hand_off(ch.CPH, ch.RPW, ch.RANG);  // the exact terms
 }
 
 // Undoes the last proposal (objects ka, kb): the backed-up poses and FocalPoint terms, the
@@ -1083,14 +1090,15 @@ __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, in
     for (int q = nb - 1; q >= 0; --q) {
         const DBackup b = ch.aux->b[q];
         write_pose<S>(ch, o, r, writer, b.k, b.x, b.y, b.ry);
-        if (writer) ch.CPH[b.k] = b.w;
+        if (writer) stage(ch.CPH).put(b.k, b.w);
     }
     for (int w = r; w < ch.SW; w += L) {
         const uint32_t t = ch.SAM[w];
-        ch.SAM[w] = ch.SAMB[w];
-        ch.SAMB[w] = t;
+        stage(ch.SAM).put(w, ch.SAMB[w]);
+        stage(ch.SAMB).put(w, t);
     }
-    wave_sync();
+    // the restored poses, boxes, FocalPoint terms and SurfaceArea bits
+    hand_off(ch.X, ch.Y, ch.BOX, ch.RYF, ch.CPH, ch.SAM, ch.SAMB);
     // The Clearance row words the proposal overwrote in registers (clearances < 64) are swapped
     // back, not recomputed (a swap: a second undo re-applies the proposal's), and a clearance
     // whose source moved takes its box at the restored pose; rooms of more than 64 clearances,
@@ -1106,7 +1114,7 @@ __device__ __forceinline__ void undo_proposal(const DeltaPtrs& ch, Own<S>& o, in
         clearance_delta<S>(ch, o, n, c, ka, kb, r);
     }
     rels_undo(ch, nr, ka, kb, r, rbk);
-    wave_sync();
+    hand_off(ch.CLA, ch.NZ, ch.RPW, ch.RANG);  // the restored pairs and relationship terms
 }
 
 // ---- the kernel ---------------------------------------------------------------------------
@@ -1173,22 +1181,22 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
     ch.ONES = reinterpret_cast<const float*>(lds + lay.h_ones);
     ch.ZERO = reinterpret_cast<const double*>(lds + lay.h_zero);
     ch.ZEROF = reinterpret_cast<const float*>(lds + lay.h_zero + round16(8 * lay.DL));
-    ch.X = reinterpret_cast<double*>(base + lay.X);
-    ch.Y = reinterpret_cast<double*>(base + lay.Y);
-    ch.BOX = reinterpret_cast<float4*>(base + lay.BOX);
-    ch.RYF = reinterpret_cast<float*>(base + lay.RYF);
-    ch.CPH = reinterpret_cast<float*>(base + lay.CPH);
-    ch.NMX = reinterpret_cast<float*>(base + lay.NMX);
+    ch.X = {reinterpret_cast<double*>(base + lay.X)};
+    ch.Y = {reinterpret_cast<double*>(base + lay.Y)};
+    ch.BOX = {reinterpret_cast<float4*>(base + lay.BOX)};
+    ch.RYF = {reinterpret_cast<float*>(base + lay.RYF)};
+    ch.CPH = {reinterpret_cast<float*>(base + lay.CPH)};
+    ch.NMX = {reinterpret_cast<float*>(base + lay.NMX)};
     const int np = lay.NP;
-    ch.CLA = reinterpret_cast<float4*>(base + lay.CLA);
-    ch.NZ = reinterpret_cast<uint64_t*>(base + lay.NZ);
-    ch.SAM = reinterpret_cast<uint32_t*>(base + lay.SAM);
-    ch.SAMB = reinterpret_cast<uint32_t*>(base + lay.SAMB);
-    ch.RPW = reinterpret_cast<double*>(base + lay.RPW);
-    ch.RANG = reinterpret_cast<double*>(base + lay.RANG);
-    ch.LCL = reinterpret_cast<float*>(base + lay.LCL);
-    ch.LSA = reinterpret_cast<float*>(base + lay.LSA);
-    ch.aux = reinterpret_cast<DeltaAux*>(base + lay.AUX);
+    ch.CLA = {reinterpret_cast<float4*>(base + lay.CLA)};
+    ch.NZ = {reinterpret_cast<uint64_t*>(base + lay.NZ)};
+    ch.SAM = {reinterpret_cast<uint32_t*>(base + lay.SAM)};
+    ch.SAMB = {reinterpret_cast<uint32_t*>(base + lay.SAMB)};
+    ch.RPW = {reinterpret_cast<double*>(base + lay.RPW)};
+    ch.RANG = {reinterpret_cast<double*>(base + lay.RANG)};
+    ch.LCL = {reinterpret_cast<float*>(base + lay.LCL)};
+    ch.LSA = {reinterpret_cast<float*>(base + lay.LSA)};
+    ch.aux = {reinterpret_cast<DeltaAux*>(base + lay.AUX)};
     ch.W = lay.W;
     ch.SW = lay.SW;
     ch.cap_cl = lay.cap_cl;
@@ -1228,25 +1236,26 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             ryf = (float)src[F_RY * n + i];
             box = shape_box(objs_l[i], (float)x, (float)y);
         }
-        ch.BOX[i] = box;
-        ch.RYF[i] = ryf;
-        ch.CPH[i] = 0.0f;
-        ch.X[i] = x;
-        ch.Y[i] = y;
-        ch.NMX[i] = 0.0f;
+        stage(ch.BOX).put(i, box);
+        stage(ch.RYF).put(i, ryf);
+        stage(ch.CPH).put(i, 0.0f);
+        stage(ch.X).put(i, x);
+        stage(ch.Y).put(i, y);
+        stage(ch.NMX).put(i, 0.0f);
     }
     for (int q = r; q < nrp; q += L) {
-        ch.RPW[q] = 0.0;
-        ch.RANG[q] = 0.0;
+        stage(ch.RPW).put(q, 0.0);
+        stage(ch.RANG).put(q, 0.0);
     }
-    for (int w = r; w < ch.SW; w += L) ch.SAM[w] = 0u;
-    wave_sync();
+    for (int w = r; w < ch.SW; w += L) stage(ch.SAM).put(w, 0u);
+    // the staged configuration and the streams' zero tails
+    hand_off(ch.BOX, ch.RYF, ch.CPH, ch.X, ch.Y, ch.NMX, ch.RPW, ch.RANG, ch.SAM);
     int wild = 0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {
         const int i = t * L + r;
         if (i < n) {
-            ch.CPH[i] = -focal_cos(*rm_l, o.xf[t], o.yf[t], (float)o.ry[t]);
+            stage(ch.CPH).put(i, -focal_cos(*rm_l, o.xf[t], o.yf[t], (float)o.ry[t]));
             wild += wild_pose(ch.X[i], ch.Y[i], o.ry[t]) ? 1 : 0;
         }
     }
@@ -1264,7 +1273,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         }
     }
     for (int ci = r; ci < c; ci += L) cla_put<S>(ch, o, ci, cla_box(ch, ci));
-    wave_sync();
+    hand_off(ch.CPH, ch.SAM, ch.CLA);  // FocalPoint terms, SurfaceArea bits, clearance boxes
     for (int ci = 0; ci < c; ++ci) nz_row<S>(ch, o, n, ci, r);
     ClRow rc_cur = cl_row0<S>(ch, o, c, r, true);  // (the current configuration's first rows)
     rels_delta(ch, nr, -2, -1, r);
@@ -1273,7 +1282,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         slot_put<S>(o.cmx, i >> 6, s.mx, r == (i & 63));
         slot_put<S>(o.carg, i >> 6, s.arg, r == (i & 63));
     }
-    wave_sync();
+    hand_off(ch.NZ, ch.RPW, ch.RANG);  // the pair rows and the relationship terms
 
     const ChainMeta m0 = a.meta[chain];
     const bool writer = r == 0;
@@ -1304,11 +1313,12 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
 
 #pragma clang loop unroll(disable)
     for (int it = 0; it < a.iterations; ++it) {
-        for (int w = r; w < ch.SW; w += L) ch.SAMB[w] = ch.SAM[w];
+        for (int w = r; w < ch.SW; w += L) stage(ch.SAMB).put(w, ch.SAM[w]);
         rng_prepare(rng);
         const int2 kk = propose<S>(rng, *rm_l, frozen, ch, o, r, writer);
         const int ka = kk.x, kb = kk.y;
-        wave_sync();
+        // the proposal's poses and boxes, its undo record, the SurfaceArea bits' backup
+        hand_off(ch.X, ch.Y, ch.BOX, ch.RYF, ch.aux, ch.SAMB);
         // Objects ka (lane 0) and kb (lane 1): FocalPoint term, SurfaceArea bits, wildness.
         int dwild = 0;
         const double rka = obj_ry<S>(o, ka < 0 ? 0 : ka), rkb = obj_ry<S>(o, kb < 0 ? 0 : kb);
@@ -1328,7 +1338,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
                     w = cph_est(atan2_est(fy, fx), p, ambo);
                 }
                 if (ambo) w = focal_cos(*rm_l, p.xf, p.yf, p.rotYf);
-                ch.CPH[k] = -w;
+                stage(ch.CPH).put(k, -w);
                 kest = !ambo;
                 const float4 vo = comp_overlaps(*rm_l, ch.BOX[k]);
                 sam_put(ch, c + k, nonzero4(vo));
@@ -1352,7 +1362,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             if (kb >= 0 && r == (kb & 63))
                 est.obj = eb ? (est.obj | (1u << (kb >> 6))) : (est.obj & ~(1u << (kb >> 6)));
         }
-        wave_sync();
+        hand_off(ch.CPH, ch.SAM);  // the moved objects' FocalPoint terms and SurfaceArea bits
         DSTAMP(0);
         typename Own<S>::wvec bk_nz = o.nz0;  // (the undo's record, undo_proposal)
         const bool chg0 = clearance_delta<S>(ch, o, n, c, ka, kb, r);
@@ -1361,7 +1371,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
         rels_delta(ch, nr, ka, kb, r, &rbk, TRACK ? nullptr : &est);
         DSTAMP(2);
         symmetry_delta<S>(ch, o, n, ka, kb, wild_star > 0, r);
-        wave_sync();
+        hand_off(ch.CLA, ch.NZ, ch.RPW, ch.RANG);  // the proposal's pairs and relationship terms
         DSTAMP(3);
         // Plain chains: Accept's uniform (the next draw after the proposal's, Kernel.cu:710) is
         // drawn first. The Clearance and SurfaceArea lists are built with the bound's partial
@@ -1543,8 +1553,8 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
             const DBackup p1 = read_obj<S>(ch, o, nb > 1 ? ch.aux->b[1].k : 0);
             undo_proposal<S>(ch, o, n, c, nr, ka, kb, r, writer, rbk, bk_nz, est, est_bk);
             if (writer) {
-                if (nb > 0) ch.aux->b[0] = p0;
-                if (nb > 1) ch.aux->b[1] = p1;
+                if (nb > 0) stage(ch.aux)->b[0] = p0;
+                if (nb > 1) stage(ch.aux)->b[1] = p1;
             }
             if constexpr (!TRACK) fix_estimates<S>(ch, o, est, r);  // (the current configuration's)
             lcl = build_cl_list<S>(ch, o, c, r, 0);
@@ -1601,7 +1611,7 @@ __global__ void __launch_bounds__(64 * delta_max_waves_s(S)) mh_delta_kernel(Lau
                 for (int k = 0; k < 8; ++k) cur[k] = uniform_f(sc[k]);
             }
             if (writer) commit_swap_zrr(ch, n);
-            wave_sync();
+            hand_off(ch.aux);  // (the step's undo record is read no more)
         }
         DSTAMP(6);
     }

@@ -201,3 +201,24 @@ def test_debug_math_buffer_sized_from_probe(mh, orc):
         mh.debug_math(1, 0, 4, 1)  # a sincos probe writes 2
     with pytest.raises(ValueError):
         mh.debug_math(mh.MH_PROBE_COUNT, 0, 4)
+
+
+def test_cross_lane_lds_hand_offs_are_named():
+    """Every cross-lane LDS hand-off of the kernels goes through mh_common.h's views (VERDICT round
+    5, item 6): no bare wave_sync() outside mh_common.h; the full-evaluation and incremental
+    kernels' chain arrays are Published members (a plain assignment to one does not compile, a
+    write goes through stage()), and each of their phases ends in a hand_off() naming arrays."""
+    csrc = ROOT / "metropolis-hastings-gpgpu_amd" / "csrc"
+    for f in sorted(csrc.iterdir()):
+        if f.suffix in (".hip", ".cpp") or (f.suffix == ".h" and f.name != "mh_common.h"):
+            src = f.read_text()
+            assert not re.search(r"\bwave_sync\s*\(\s*\)", src), f"bare wave_sync() in {f.name}"
+    chain = (csrc / "mh_chain.hip").read_text()
+    delta = (csrc / "mh_delta.hip").read_text()
+    for src, struct, arrays in ((chain, "ChainPtrs", ("P", "PX", "LCL", "CLA", "NZ", "aux")),
+                                (delta, "DeltaPtrs", ("X", "BOX", "CPH", "LCL", "SAM", "aux"))):
+        body = src[src.index(f"struct {struct} {{"):]
+        body = body[:body.index("};")]
+        for a in arrays:
+            assert re.search(rf"Published<[\w]+> [^;]*\b{a}\b", body), f"{struct}.{a} not Published"
+        assert len(re.findall(r"\bhand_off\(ch\.", src)) >= 10
