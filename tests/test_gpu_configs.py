@@ -201,6 +201,46 @@ def test_every_chain_short(mh, orc, hiplib, name, n, chains, offset):
     _check_summary(f"{name} ({steps} steps)", summ, costs, offset=offset)
 
 
+LONG = pytest.mark.skipif(not os.environ.get("MH_LONG_PARITY"),
+                          reason="long parity run (~3 min each): set MH_LONG_PARITY=1")
+
+
+@LONG
+def test_config3_every_chain_1000_steps(mh, orc, hiplib):
+    """Every one of config 3's 65,536 chains for a whole 1,000-step launch (the 20-step run above
+    is too short to reach the bound's rare paths in proportion: ~1.5% of steps are open and
+    ~0.8% recompute the current configuration exactly, so every chain takes them ~20 times
+    here), bit for bit against the oracle. Opt-in ($MH_LONG_PARITY=1): ~2.5 min of oracle time on
+    16 host threads; its record is committed under profiles/."""
+    room = mh.synthetic_room(64)
+    chains, steps, seed = 65536, 1000, 42
+    with mh.Session(room, chains, seed=seed) as s, _fast_oracle(orc):
+        s.run(steps)
+        ref_pts, ref_costs, ref_acc = orc.run_chains(room, chains, steps, seed,
+                                                     threads=HOST_THREADS)
+        s.finalize()
+        pts, costs = s.download()
+        summ = s.summary()
+    check_chains(f"config 3 (N=64, all {chains} chains x {steps} steps)", pts, costs, ref_pts,
+                 ref_costs, report=True)
+    assert summ.accepted == int(np.asarray(ref_acc).sum())
+
+
+@LONG
+def test_config5_full_length_256_sampled(mh, orc, hiplib):
+    """Config 5 at its full 10,000 steps with 256 chains sampled by global id (4x the default
+    test's 64), 32 blocks of 8 across the id range. Opt-in ($MH_LONG_PARITY=1)."""
+    room = mh.synthetic_room(256)
+    chains, steps, seed = 32768, 10_000, 42
+    starts = _spread(chains, 32, 8)
+    pts, costs, summ, sp, sc, rp, rc, ids = _session_sampled(
+        mh, orc, room, chains, steps, seed, starts, 8, 1)
+    assert len(set(ids.tolist())) == 256
+    check_chains("config 5 (N=256, 32768 x 10k, 256 sampled)", sp, sc, rp, rc, ids=ids,
+                 report=True)
+    _check_summary("config 5", summ, costs)
+
+
 def test_config4_every_chain_all_shards(mh, orc, hiplib):
     """Config 4's whole population: all 524,288 global ids, as the 8 ranks of the 8-GPU run
     shard them (rank r: a 65,536-chain session with chain_offset r * 65,536, Kernel.cu:950 one

@@ -10,4 +10,4 @@ mkdir -p abvar build/var
 F="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -mllvm -disable-machine-licm -Wno-unused-result"
 /opt/rocm/bin/hipcc $F -Imetropolis-hastings-gpgpu_amd/csrc "$@" -c ${MH_CHAIN_SRC:-metropolis-hastings-gpgpu_amd/csrc/mh_chain.hip} -o build/var/chain_$NAME.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/var/chain_$NAME.o build/mh_chain_xw.hip.o \
-  build/mh_chain_best.hip.o build/mh_delta.hip.o build/mh_abi.cpp.o -o abvar/libmhgpu_$NAME.so
+  build/mh_chain_best.hip.o build/mh_delta.hip.o build/mh_spec.hip.o build/mh_abi.cpp.o -o abvar/libmhgpu_$NAME.so
