@@ -1063,12 +1063,14 @@ enum { BOUND_OPEN = 0, BOUND_REJECT = 1, BOUND_ACCEPT = 2 };
 // three of the four roundings of W * component on either side); and the decision's own
 // arithmetic on t, e and cur (t + 1.25 e, minus cur, the star ends): 8 U cabs + 3 U (|o1| +
 // |o2|) + 3 U (|t| + |cur|) covers them.
+// The lane parts of the eight sums bound_decide composes, from this lane's terms (below). Each
+// part is a sum of per-component contributions, so lanes (or wavefronts) holding different
+// components of one configuration may each call it with the others' fields zero and add their
+// parts (the speculative kernel's two wavefronts per node): the additions' extra roundings stay
+// within the tree allowance's six levels. `part[7]` takes the angle allowances scaled by 1 / cr.
 template <bool DPW = false>
-__device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
-                                            const BoundTerms& bt, float u, CostIv cur,
-                                            CostIv& star, float slack = 1.0f) {
-    // (fused multiply-adds allowed here: every rounding below is counted in the allowance, and
-    // a fused operation rounds once where the count assumes two)
+__device__ __forceinline__ void bound_parts(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                            const BoundTerms& bt, float (&part)[8]) {
 #pragma clang fp contract(fast)
     constexpr float U = 0x1p-24f;
     const float kf = (float)bt.k;
@@ -1101,11 +1103,30 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     // otherwise
     // (eang / cr32 from the hardware reciprocal, 1 ulp, raised by 8 U: never below the quotient)
     const float icr = __builtin_amdgcn_rcpf(cr32) * (1.0f + 8.0f * U);
-    const float part[8] = {bt.nx, bt.ny, bt.pw, bt.ang, lin, elin,
-                           bt.anx + bt.any + (DPW ? 0.0f : alin),
-                           bt.aang + (DPW ? alin : bt.eang * icr)};
-    float sum[8];
-    wave_fsum8(part, sum);
+    part[0] = bt.nx;
+    part[1] = bt.ny;
+    part[2] = bt.pw;
+    part[3] = bt.ang;
+    part[4] = lin;
+    part[5] = elin;
+    part[6] = bt.anx + bt.any + (DPW ? 0.0f : alin);
+    part[7] = bt.aang + (DPW ? alin : bt.eang * icr);
+}
+
+// The proposal's total estimate and decision from the eight sums of bound_parts (fp32 path:
+// the PairWise and PairWiseAngle sums in sum[2], sum[3]; with DPW their fp64 sums come from the
+// wavefront's lanes' bt.pwd, bt.angd, and the estimated angle terms' allowances from bt.eang).
+// Returns BOUND_REJECT / BOUND_ACCEPT / BOUND_OPEN for this lane (the caller makes it uniform)
+// and the proposal's interval in `star`.
+template <bool DPW = false>
+__device__ __forceinline__ int bound_compose(const DevRoom& rm, int n, int nrel, int k, int pwx,
+                                             const float (&sum)[8], const BoundTerms& bt, float u,
+                                             CostIv cur, CostIv& star, float slack) {
+#pragma clang fp contract(fast)
+    constexpr float U = 0x1p-24f;
+    const float kf = (float)k;
+    const float eacc = 0x1p-29f * (float)(n + nrel);
+    const float cr32 = (26.0f + kf + eacc + (float)pwx) * U;
     const float s_nx = sum[0], s_ny = sum[1], s_lin = sum[4], s_elin = sum[5];
     const float a_nx = fmaxf(fabsf(s_nx), sum[6]), a_ny = fmaxf(fabsf(s_ny), sum[6]),
                 a_ang = fmaxf(fabsf(sum[3]), sum[7]);
@@ -1137,13 +1158,13 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
         // like the reference's (float)(pw * ang), to float
         const double spw = wave_dsum(bt.pwd), sang = wave_dsum(bt.angd);
         const double pad = spw * sang;
-        const float cr = (float)((double)(nrel + bt.k + 12) * 0x1p-53);
+        const float cr = (float)((double)(nrel + k + 12) * 0x1p-53);
         float epw = cr * (float)fabs(spw) * (1.0f + 64.0f * U),
               eang = cr * a_ang * (1.0f + 64.0f * U);
-        if (bt.pwx) {  // (uniform) estimated relationship terms (the incremental kernel's
-                       // EstState): kPwEstU U relative on PairWise, eang each on the angles; the
-                       // fp32 tree sum of the allowances raised by 8 U, 64 U on the relative part
-            epw += (float)bt.pwx * U * (float)fabs(spw) * (1.0f + 64.0f * U);
+        if (pwx) {  // (uniform) estimated relationship terms (the incremental kernel's
+                    // EstState): kPwEstU U relative on PairWise, eang each on the angles; the
+                    // fp32 tree sum of the allowances raised by 8 U, 64 U on the relative part
+            epw += (float)pwx * U * (float)fabs(spw) * (1.0f + 64.0f * U);
             eang += wave_fsum(bt.eang) * (1.0f + 8.0f * U);
         }
         pa = (float)pad;
@@ -1177,8 +1198,36 @@ __device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int
     const bool acc = u < 1.0f && (xl >= 0.0f || (xl > -23.9f && lu < xl - 1e-4f));
     star.lo = t - 1.5f * e;
     star.hi = t + 1.5f * e;
+    return rej ? BOUND_REJECT : (acc ? BOUND_ACCEPT : BOUND_OPEN);
+}
+
+// Whether Accept's decision for this proposal is already certain, for a chain that owns the
+// wavefront: BOUND_REJECT / BOUND_ACCEPT, or BOUND_OPEN (the exact costs are needed). n objects,
+// c clearances, nrel relationships, ncl non-zero Clearance terms; `cur` holds the current
+// total. The arithmetic after the lane sums is fp32 on wave-uniform values (with DPW the
+// PairWise and PairWiseAngle sums and their product are fp64: their fp32 error dominated the
+// bound at N = 256, where PairWise is most of the total); the proposal's exact total lies in
+// t +- 1.25 e. `star` receives an interval around it that also absorbs the rounding of its own
+// ends (e >= 8 U |t|, so 0.25 e does).
+//
+// e is the sum of term-by-term error bounds: each sum's (the reference's sequential rounding
+// and this estimate's), each composition step of Costs() (the e1, e2 and 12 U terms), and the
+// roundings no term covers -- the reference's five float additions of the total (:547), each
+// at most U times a partial sum of the components, whose magnitudes add up to at most cabs
+// below; the two additions forming t; the weight products' second rounding (e1 and e2 count
+// three of the four roundings of W * component on either side); and the decision's own
+// arithmetic on t, e and cur (t + 1.25 e, minus cur, the star ends): 8 U cabs + 3 U (|o1| +
+// |o2|) + 3 U (|t| + |cur|) covers them. (The arithmetic: bound_parts and bound_compose.)
+template <bool DPW = false>
+__device__ __forceinline__ int bound_decide(const DevRoom& rm, int n, int c, int nrel, int ncl,
+                                            const BoundTerms& bt, float u, CostIv cur,
+                                            CostIv& star, float slack = 1.0f) {
+    float part[8], sum[8];
+    bound_parts<DPW>(rm, n, c, nrel, ncl, bt, part);
+    wave_fsum8(part, sum);
+    const int d = bound_compose<DPW>(rm, n, nrel, bt.k, bt.pwx, sum, bt, u, cur, star, slack);
     // the chain's first lane decides, so the decision is wave-uniform by construction
-    return __builtin_amdgcn_readfirstlane(rej ? BOUND_REJECT : (acc ? BOUND_ACCEPT : BOUND_OPEN));
+    return __builtin_amdgcn_readfirstlane(d);
 }
 
 // Whether Accept certainly rejects this proposal (bound_decide with an exact current total).
