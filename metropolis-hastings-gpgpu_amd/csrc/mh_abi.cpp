@@ -232,6 +232,7 @@ struct Geometry {
     bool few;            // step with OP_STEP_FEW (no register cap: too few chains to use it)
     bool spec;           // step with the speculative kernel (mh_spec.hip)
     int spec_h;          // its halves: 2 (16-node tree, 4 wavefronts per chain) or 1 (8, 2)
+    bool spec_bound;     // its instance deciding on the bound where certain (177 VGPRs: 4 chains per CU)
     mh::ChainLds lay;    // init / step
     int waves_ol;
     mh::ChainLds lay_ol; // final / evaluation (with the OffLimits boxes)
@@ -332,6 +333,14 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
     g.spec_h = n_chains <= 2LL * cus ? 2 : 1;
     if (const char* e = getenv("MH_SPEC_H"))
         if (*e) g.spec_h = atoi(e) >= 2 ? 2 : 1;
+    // Decisions on the bound (mh_spec.hip): the instance that takes them holds ~175 VGPRs, two
+    // wavefronts per SIMD (4 chains per CU at one half, 2 at two), and its batches trade the exact
+    // jobs and sums for fp32 estimates. Measured at N = 8 (ms per 1,000-step launch, bound / exact,
+    // profiles/r06/r06i_*): 256 chains 1.530 / 1.560, 1,024 chains 2.525 / 1.979. So up to two chains
+    // per CU. $MH_SPEC_BOUND=0/1 forces it.
+    g.spec_bound = n_chains <= 2LL * cus;
+    if (const char* e = getenv("MH_SPEC_BOUND"))
+        if (*e) g.spec_bound = atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);
     g.waves_ol = 4;
     while (g.waves_ol > 1 && mh::lds_bytes(g.lay_ol, g.L, g.waves_ol) > 80 * 1024) g.waves_ol >>= 1;
@@ -465,6 +474,7 @@ struct mh_session {
         a.n_temps = n_temps;
         a.ladder = d_ladder;
         a.bound_slack = bound_slack();
+        a.spec_bound = geo.spec_bound ? 1 : 0;
         a.lay = geo.lay;
         a.dlay = geo.dlay;
         return a;
@@ -546,7 +556,8 @@ bool record_done(mh_session* s, hipStream_t st) {
 // made after one of them changed runs the kernel it names, not the previous call's.
 std::string geometry_env() {
     static const char* const kVars[] = {"MH_LANES", "MH_WAVES", "MH_STEP_FEW", "MH_SPEC",
-                                        "MH_SPEC_H", "MH_DELTA", "MH_DELTA_WAVES"};
+                                        "MH_SPEC_H", "MH_SPEC_BOUND", "MH_DELTA",
+                                        "MH_DELTA_WAVES"};
     std::string key;
     for (const char* v : kVars) {
         const char* e = getenv(v);
@@ -1264,7 +1275,7 @@ MH_API int mh_session_occupancy(const mh_session* s, int* chains_per_cu) {
     const auto& g = s->geo;
     int blocks = 0;
     if (g.spec) {
-        *chains_per_cu = mh::spec_blocks_per_cu(g.spec_h) * mh::spec_waves();
+        *chains_per_cu = mh::spec_blocks_per_cu(g.spec_h, g.spec_bound) * mh::spec_waves();
     } else if (g.delta) {
         blocks = mh::delta_blocks_per_cu(s->room.rm.n, g.dwaves,
                                          mh::delta_lds_bytes(s->geo.dlay, g.dwaves));

@@ -927,9 +927,9 @@ __device__ MH_EVAL_ATTR void eval_costs(const LaunchArgs& a, const ChainPtrs& ch
             if (r == 0) MH_PHASE(ch, 4, t0);
 #if MH_STAMPS
             if (r == 0) {
-                ch.aux->cyc[8] += 1;
-                ch.aux->cyc[9] += d == BOUND_REJECT ? 1 : 0;
-                ch.aux->cyc[10] += d == BOUND_ACCEPT ? 1 : 0;
+                stage(ch.aux)->cyc[8] += 1;
+                stage(ch.aux)->cyc[9] += d == BOUND_REJECT ? 1 : 0;
+                stage(ch.aux)->cyc[10] += d == BOUND_ACCEPT ? 1 : 0;
             }
 #endif
             if (d == BOUND_REJECT) {
@@ -1729,7 +1729,7 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
                         if (nb > 1) ax->b[1] = s1;
                     }
 #if MH_STAMPS
-                    if (writer) ch.aux->cyc[11] += 1;
+                    if (writer) stage(ch.aux)->cyc[11] += 1;
 #endif
                     cur_total = uniform_f(cx[0]);
                     cur_exact = true;

@@ -1119,9 +1119,9 @@ __device__ __forceinline__ void bound_parts(const DevRoom& rm, int n, int c, int
 // Returns BOUND_REJECT / BOUND_ACCEPT / BOUND_OPEN for this lane (the caller makes it uniform)
 // and the proposal's interval in `star`.
 template <bool DPW = false>
-__device__ __forceinline__ int bound_compose(const DevRoom& rm, int n, int nrel, int k, int pwx,
-                                             const float (&sum)[8], const BoundTerms& bt, float u,
-                                             CostIv cur, CostIv& star, float slack) {
+__device__ __forceinline__ float bound_te(const DevRoom& rm, int n, int nrel, int k, int pwx,
+                                          const float (&sum)[8], const BoundTerms& bt, CostIv cur,
+                                          float slack, float& e_out) {
 #pragma clang fp contract(fast)
     constexpr float U = 0x1p-24f;
     const float kf = (float)k;
@@ -1182,8 +1182,16 @@ __device__ __forceinline__ int bound_compose(const DevRoom& rm, int n, int nrel,
     const float t = (o1 + o2) + s_lin;
     const float acur = fmaxf(fabsf(cur.lo), fabsf(cur.hi));
     const float cabs = fabsf(o1) + e1 + fabsf(o2) + e2 + (DPW ? sum[7] : sum[6]);
-    const float e = slack * (e1 + e2 + s_elin + 3.0f * U * (fabsf(o1) + fabsf(o2)) +
-                             8.0f * U * cabs + 3.0f * U * (fabsf(t) + acur));
+    e_out = slack * (e1 + e2 + s_elin + 3.0f * U * (fabsf(o1) + fabsf(o2)) +
+                     8.0f * U * cabs + 3.0f * U * (fabsf(t) + acur));
+    return t;
+}
+
+// Accept's decision for a proposal whose exact total lies in t +- 1.25 e (bound_te, e computed
+// for a current total of the magnitude of `cur`'s: the decision's own arithmetic on it), against
+// the current total's interval `cur`; the proposal's interval in `star` (below).
+__device__ __forceinline__ int bound_vs(float t, float e, float u, CostIv cur, CostIv& star) {
+#pragma clang fp contract(fast)
     const float x = (float)kBeta * ((t + 1.25f * e) - cur.lo);   // beta (star - cur), upper end
     const float xl = (float)kBeta * ((t - 1.25f * e) - cur.hi);  // and lower end
     // log(u) from the f32 log: within 1e-5 of the true value for u in [2^-33, 1]; 1e-4 margin
@@ -1199,6 +1207,15 @@ __device__ __forceinline__ int bound_compose(const DevRoom& rm, int n, int nrel,
     star.lo = t - 1.5f * e;
     star.hi = t + 1.5f * e;
     return rej ? BOUND_REJECT : (acc ? BOUND_ACCEPT : BOUND_OPEN);
+}
+
+template <bool DPW = false>
+__device__ __forceinline__ int bound_compose(const DevRoom& rm, int n, int nrel, int k, int pwx,
+                                             const float (&sum)[8], const BoundTerms& bt, float u,
+                                             CostIv cur, CostIv& star, float slack) {
+    float e;
+    const float t = bound_te<DPW>(rm, n, nrel, k, pwx, sum, bt, cur, slack, e);
+    return bound_vs(t, e, u, cur, star);
 }
 
 // Whether Accept's decision for this proposal is already certain, for a chain that owns the

@@ -41,6 +41,8 @@ struct LaunchArgs {
     int n_temps;             // parallel tempering replicas per group (1 = off)
     const double* ladder;    // [n_temps] inverse temperatures (n_temps > 1)
     unsigned int* xw;        // [n_chains][6] XORWOW states {d, x0..x4} (rng == RNG_CURAND_XORWOW)
+    int spec_bound;          // speculative kernel: decide on the bound where it is certain
+                             // (1, default; $MH_SPEC_BOUND=0: every node's exact costs)
     float bound_slack;       // diagnostic: widens the step bound's error allowance ($MH_BOUND_SLACK,
                              // default 1; the tests use it to send many steps down the exact paths)
     ChainLds lay;
@@ -72,7 +74,7 @@ bool spec_fits(int n, int c, int r);
 int spec_waves();                       // chains per workgroup of the speculative kernel
 int spec_waves_per_chain(int halves);   // its wavefronts per chain
 size_t spec_lds_bytes(int halves);
-int spec_blocks_per_cu(int halves);
+int spec_blocks_per_cu(int halves, bool bound);
 hipError_t launch_spec(const LaunchArgs& a, int halves, hipStream_t s);
 hipError_t launch_xorwow_init(uint64_t seed, int64_t chain_offset, int64_t n, unsigned int* xw,
                               hipStream_t s);

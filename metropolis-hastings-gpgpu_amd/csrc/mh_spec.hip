@@ -36,6 +36,9 @@ __device__ unsigned long long g_spec_cycles[16];
 #define SSTAMP(k) do { } while (0)
 #endif
 
+#if MH_CHECK
+static __device__ unsigned int g_spec_ck[12];  // (check builds) the first wrong certain decision's inputs
+#endif
 namespace mh {
 namespace {
 
@@ -81,10 +84,15 @@ __device__ __forceinline__ int rec_k2(int code) { return ((code >> 6) & 15) - 1;
 __device__ __forceinline__ int rec_h(int code) { return (code >> 10) & 1; }
 
 struct SpecW0 {  // LDS of a half's chain wavefront
-    double S[K][S_W0];            // each group's streams
+    double S[K][S_W0];            // each group's streams (batches decided on the bound: the
+                                  // node's FocalPoint and relationship terms, estimates or
+                                  // exact, in S_FP / S_PW / S_ANG and the angle terms'
+                                  // allowances in the VisualBalance slots, for its commit)
     double RY[K][GL];             // each group's double rotY of every object (Symmetry, :305)
     double XD[K][GL], YD[K][GL];  // each group's double x, y (wave 1's symmetry and boxes)
     ObjP P[K][GL];                // each group's float pose words
+    float EO[K][GL];              // (bound batches) each object's FocalPoint allowance: 0 for an
+                                  // exact term, kDeltaCph for an estimate
 };
 
 struct SpecW1 {  // LDS of a half's list wavefront
@@ -92,33 +100,42 @@ struct SpecW1 {  // LDS of a half's list wavefront
     float4 CLB[K][GL];       // each group's clearance boxes at their sources (:414-415)
 };
 
+// A node's bound (batches decided on the bound): the eight sums of bound_parts over its chain
+// wavefront's lanes, the three its list wavefront contributes (lin, elin, alin: parts 4-6), and
+// the node's PairWise estimate flag (pwx, as a float).
+constexpr int kBS = 12;
 template <int H>
 struct SpecShared {  // LDS of the chain shared by its wavefronts
     double SUM[2][K * H][8];  // each node's eight sums (double-buffered by batch parity)
+    float BS[K * H][kBS];     // each node's bound sums (written before the sums barrier, read
+                              // after it and before the next views barrier)
     StepRec ring[kRing];  // the step records (wave 1 writes, the chain wavefronts read)
     unsigned int wd[128];  // the 128-word window of the Philox stream being parsed (wave 1)
     unsigned int produced;  // records written so far (wave 1; read by wave 0 between the barriers)
     unsigned int consumed;  // records committed so far (wave 0; read by wave 1 between them)
     int stop;             // wave 0 to the others: the chain's steps are done
+    int exact;            // wave 0 to the others: this batch evaluates every node's exact costs
 };
 
 struct SpecHdr {  // LDS of the workgroup: the room tables
     RectShape objs[GL];  // off-limits rectangles (pad: area bits)
     RectShape clrs[GL];  // clearance rectangles (pad: source object)
     RelConst rel[RMAX];
+    float4 re0[RMAX], re1[RMAX];  // the relationships' fp32 estimate constants (rel_est_consts)
 };
 
 constexpr int round16s(size_t v) { return (int)((v + 15) & ~(size_t)15); }
 constexpr int kSpecHdrBytes = round16s(sizeof(SpecHdr));
 constexpr int kSpecW0Bytes = round16s(sizeof(SpecW0));
 constexpr int kSpecW1Bytes = round16s(sizeof(SpecW1));
-// LDS per chain: H = 1 22.1 KB (seven chains in a CU's 160 KB), H = 2 37.1 KB (four)
+// LDS per chain: H = 1 23.2 KB (seven chains in a CU's 160 KB), H = 2 38.8 KB (four)
 template <int H>
 constexpr int spec_bytes() {
     return kSpecHdrBytes + H * (kSpecW0Bytes + kSpecW1Bytes) + round16s(sizeof(SpecShared<H>));
 }
 static_assert(sizeof(StepRec) == 32, "StepRec");
 static_assert(spec_bytes<2>() * 4 <= 160 * 1024, "four 16-node chains per CU");
+static_assert(spec_bytes<1>() * 7 <= 160 * 1024, "seven 8-node chains per CU");
 
 // A Philox word past the LDS window (frozen-object redraws only): out of line, value-only.
 __device__ __attribute__((noinline)) unsigned int philox_far(uint64_t seed, uint64_t sub,
@@ -191,6 +208,14 @@ __device__ __forceinline__ float sym_row(const ObjP* P, const double* RY, int n,
         }
     }
     return best;
+}
+
+// Sum of v over this lane's group of 8 (every lane of the group gets it): three DPP levels.
+__device__ __forceinline__ float grp8_fsum(float v) {
+    v += bfly<1>(v);
+    v += bfly<2>(v);
+    v += bfly<4>(v);
+    return v;
 }
 
 // Appends the non-zero components of t (when `on`), in lane order within each group, to the
@@ -292,7 +317,7 @@ __device__ __forceinline__ int nth_bit(uint32_t m, int q) {
     return pos;
 }
 
-template <int H>
+template <int H, bool BOUND>
 __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
     constexpr int NN = K * H;  // tree nodes per batch
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -315,7 +340,11 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
         s.pad = a.clrc[i].src;
         Hd->clrs[i] = s;
     }
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) Hd->rel[i] = a.relc[i];
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+        Hd->rel[i] = a.relc[i];
+        Hd->re0[i] = a.rele[i];
+        Hd->re1[i] = a.rele[nr + i];
+    }
     __syncthreads();
 
     const int64_t chain = (int64_t)blockIdx.x;  // (the whole workgroup: one chain)
@@ -508,6 +537,9 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             const auto pv = receive_workgroup(X0->P[g], X0->RY[g], X0->XD[g], X0->YD[g]);
             if (SH->stop) break;
             cons_seen = SH->consumed;
+            // (check builds evaluate the exact costs and the bound of every batch)
+            const bool exact_b = !BOUND || SH->exact != 0 || MH_CHECK;
+            const bool bound_b = BOUND && (SH->exact == 0 || MH_CHECK);
             const ObjP* Pg = pv.a.ptr();
             const int ro = r < n ? r : 0;
             const double sx = pv.c[ro], sy = pv.d[ro], sry = pv.b[ro];
@@ -527,17 +559,64 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             }
             // Symmetry row r, Kernel.cu:292-312.
             const bool exact_mode = group_ballot<GL>(wild, gbase) != 0;
+            float rxr = 0.0f, ryr = 0.0f, rr = 0.0f;
             if (r < n) {
                 double al = sx * (double)rm.ux;
                 al = al + sy * (double)rm.uy;
                 const float sd = (float)(2.0 * (rm.along_f - al));
-                const float rxr = (float)(sx + (double)(sd * rm.ux));
-                const float ryr = (float)(sy + (double)(sd * rm.uy));
-                float rr = (float)(rm.two_focal_rot - sry);
+                rxr = (float)(sx + (double)(sd * rm.ux));
+                ryr = (float)(sy + (double)(sd * rm.uy));
+                rr = (float)(rm.two_focal_rot - sry);
                 if ((double)rr < -kPI) rr = (float)((double)rr + kTwoPI);
-                Sst.put(S_SYM + r, -(double)sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode));
+                if (exact_b)
+                    Sst.put(S_SYM + r, -(double)sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode));
             }
             const auto sv = publish(Sst, CLBst);
+            if (bound_b) {
+                // The node's bound, this wavefront's share (bound_parts): the row maximum's fp32
+                // estimate with sym_err's allowance (max(0, .) is 1-Lipschitz, and the exact row
+                // maximum lies within the estimate's allowance of the largest estimate), the
+                // lane's column of Clearance terms in clearance order, its SurfaceArea terms.
+                BoundTerms bt{};
+                bt.k = 8;
+                if (r < n) {
+                    float m1 = -INFINITY;
+                    for (int j = 0; j < n; ++j)
+                        m1 = fmaxf(m1, sym_val_fast(objp_f4(Pg[j]), rxr, ryr, rr));
+                    const float mx = fmaxf(0.0f, m1);
+                    bt.esym = sym_err(m1, rr);
+                    bt.sym = -mx;
+                    bt.symw = (float)(n - r) * (mx + bt.esym);  // (row r: position r)
+                    float cls = 0.0f;
+                    for (int i = 0; i < c; ++i) {
+                        const float ov = overlap(sv.b[i], box);
+                        cls += ov;
+                        bt.kcl += ov != 0.0f ? 1 : 0;
+                    }
+                    bt.cl = -cls;
+                }
+                bt.sa = -((sac.x + sac.y + sac.z + sac.w) + (sao.x + sao.y + sao.z + sao.w));
+                int ncl = bt.kcl;  // (the node's non-zero Clearance terms)
+                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0xB1, 0xF, 0xF, false);
+                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x4E, 0xF, 0xF, false);
+                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x141, 0xF, 0xF, false);
+                float part[8];
+                bound_parts(rm, n, c, nr, ncl, bt, part);
+                // a pose outside the range the symmetry estimate is proven for: no bound (NaN)
+                const float lin = exact_mode ? __builtin_nanf("") : part[4];
+                const float s4 = grp8_fsum(lin), s5 = grp8_fsum(part[5]), s6 = grp8_fsum(part[6]);
+                const Staged<float> B{SH->BS[K * hf + g]};
+                if (r == 0) {
+                    B.put(8, s4);
+                    B.put(9, s5);
+                    B.put(10, s6);
+                }
+            }
+            if (!exact_b) {  // (the barrier below publishes the bound's sums)
+                publish_workgroup(Staged<double>{SH->SUM[par][K * hf + g]});
+                par ^= 1;
+                continue;
+            }
             // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
             // (clearances, then objects, :445-480), compacted in the reference's order.
             int ncl = 0, nsa = 0;
@@ -594,6 +673,7 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
     const Staged<double> XDst{X0->XD[g]}, YDst{X0->YD[g]};
     const Staged<int> STOP{&SH->stop};
     const Staged<unsigned int> CONS{&SH->consumed};
+    const Staged<int> EXACT{&SH->exact};
     if (r < n) {
         ObjP p;
         p.xf = (float)cx;
@@ -688,22 +768,43 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
     };
     set_tree(0.4f);
     unsigned int batches = 0;
+    // Decisions on the bound (BOUND; mh_common.h bound_parts / bound_te): a batch first
+    // bounds every node's total from fp32 estimates -- the moved objects' FocalPoint terms and the
+    // touched relationships' terms as the full-evaluation kernel estimates them, the symmetry row
+    // maxima as their screening estimates, the other terms exact -- and decides Accept where the
+    // bound makes it certain. The realised path commits while its decisions are certain; at the
+    // first open one it stops, and the next batch evaluates every node's exact costs (as every
+    // batch does without the bound), after a refresh batch that makes the current costs exact
+    // when a certain acceptance left them an interval. The carried terms may be estimates
+    // (allowances efp_c, ea0_c, ea1_c: 0 when exact); an exact batch evaluates them exactly.
+    float efp_c = 0.0f, ea0_c = 0.0f, ea1_c = 0.0f;
+    CostIv cur_iv{cur[0], cur[0]};
+    bool cur_exact = true;
+    bool exact_next = !BOUND;
 #if MH_STAMPS
     unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
 #endif
 #pragma clang loop unroll(disable)
     for (int done = 0;;) {
-        if (done >= a.iterations) {  // (the list wavefronts leave their loop at this barrier)
+        const bool finish = done >= a.iterations;
+        if (finish && cur_exact) {  // (the list wavefronts leave their loop at this barrier)
             if (lead && lane == 0) STOP.put(0, 1);
             publish_workgroup(STOP);
             break;
         }
+        // (check builds: exact costs and the bound in every batch, decisions on the exact costs)
+        const bool exact_b = exact_next || finish || !BOUND || MH_CHECK;
+        const bool bound_b = !exact_b || MH_CHECK;
+        // a launch ends, and an exact batch starts, with the current configuration's exact
+        // costs: when a certain acceptance left them an interval, a refresh batch (no steps, every
+        // node the incoming configuration) evaluates them first
+        const bool refresh = exact_b && !cur_exact;
         if ((++batches & 31u) == 0u)
             set_tree((float)(accepted + 2u) / (float)(done + 5));
         // steps this batch can reach: the tree's depth, the launch's remaining steps, the
         // records wave 1 has written (0: a round that only waits for it)
-        const int kb = min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
+        const int kb = refresh ? 0 : min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
         if (lane < kb) {
             const StepRec& q = rec(cons + (unsigned int)lane);
             r_code = q.code;
@@ -731,17 +832,17 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             XDst.put(r, sx);
             YDst.put(r, sy);
         }
-        if (lead && lane == 0) STOP.put(0, 0);
+        if (lead && lane == 0) {
+            STOP.put(0, 0);
+            EXACT.put(0, exact_b ? 1 : 0);
+        }
         SSTAMP(1);
         const auto pv = publish_workgroup(Pst, RYst, XDst, YDst);  // (to the list wavefront too)
         SSTAMP(2);
         prod_seen = SH->produced;  // (wave 1 writes it before this barrier, never between)
         (void)pv;  // (the views are read below through Pall: every group's)
+        const Published<ObjP> Pall{&X0->P[0][0]};  // (every group's view, published above)
 
-        // The exact FocalPoint terms of the group's moved objects and the terms of the
-        // relationships they touch, the rest carried from the incoming state. The group's
-        // jobs (touched relationships first, then moved objects) are dealt out to its 8 lanes,
-        // one double atan2 per lane per pass (Kernel.cu:170-188, 222, 249-253, 271-277).
         const uint32_t mv = (uint32_t)group_ballot<GL>(moved && r < n, gbase);
         bool t0 = false, t1 = false;
         if (r < nr) {
@@ -752,111 +853,208 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             const RelConst& rc = Hd->rel[r + GL];
             t1 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
-        const uint32_t tm = (uint32_t)group_ballot<GL>(t0, gbase) |
-                            ((uint32_t)group_ballot<GL>(t1, gbase) << GL);
-        const int nrt = __builtin_popcount(tm);
         const Staged<double> Sg = Sall.at(g * S_W0);
-        if (r < n) {
-            const float area = __int_as_float(Hd->objs[r].pad);
-            Sg.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
-            Sg.put(S_VBY + r, (double)area * sy);
-            if (!moved) Sg.put(S_FP + r, -(double)cph);
-        }
-        if (r < nr && !t0) {
-            Sg.put(S_PW + r, -rpw0);
-            Sg.put(S_ANG + r, -rang0);
-        }
-        if (r + GL < nr && !t1) {
-            Sg.put(S_PW + r + GL, -rpw1);
-            Sg.put(S_ANG + r + GL, -rang1);
-        }
-        // The 8 nodes' jobs are dealt out to the wavefront's 64 lanes (one pass unless they
-        // number more than 64): lane q takes job q of the concatenation, group by group.
-        const uint32_t jw = tm | (mv << 16) | ((uint32_t)nrt << 24);  // (group-uniform)
-        uint32_t JW[K];
-        int JP[K + 1];
-        JP[0] = 0;
+        if (bound_b) {
+            // The node's bound, this wavefront's share: the VisualBalance products, the moved
+            // objects' FocalPoint terms and the touched relationships' terms as fp32 estimates
+            // (exact where an estimate cannot vouch for its branch), the rest carried.
+            float cph_n = cph, efp_n = efp_c;
+            double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
+            float ea0n = ea0_c, ea1n = ea1_c;
+            const ObjP* PGg = Pall.ptr() + g * GL;
+            if (moved && r < n) {
+                ObjP p;
+                p.xf = xf;
+                p.yf = yf;
+                p.rotYf = ryf;
+                p.pad = 0.0f;
+                const float fy = rm.fyf - yf, fx = rm.fxf - xf;
+                bool ambo = !(fmaxf(fabsf(fy), fabsf(fx)) >= 0x1p-100f);
+                cph_n = cph_est(atan2_est(fy, fx), p, ambo);
+                efp_n = kDeltaCph;
+                if (ambo) cph_n = __builtin_nanf("");  // (an invalid bound: the node is open)
+            }
+            auto rel_est = [&](int q, double& pw, double& an, float& ea) __attribute__((always_inline)) {
+                const RelConst& rc = Hd->rel[q];
+                const float4 e0 = Hd->re0[q], e1 = Hd->re1[q];
+                bool amb = false;
+                pw = rel_pw_est(e0, PGg[rc.s], PGg[rc.t], amb);
+                const ObjP as = PGg[rc.as], atp = PGg[rc.at];
+                const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
+                amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
+                an = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
+                if (amb) pw = __builtin_nan("");  // (an estimate that cannot vouch for its branch:
+                                                  // the node is open, its exact terms next batch)
+            };
+            if (t0) rel_est(r, pw0, an0, ea0n);
+            if (t1) rel_est(r + GL, pw1, an1, ea1n);
+            BoundTerms bt{};
+            bt.k = 8;
+            if (r < n) {
+                const float area = __int_as_float(Hd->objs[r].pad);
+                bt.nx = (float)((double)area * sx);  // Kernel.cu:200-201
+                bt.ny = (float)((double)area * sy);
+                bt.anx = fabsf(bt.nx);
+                bt.any = fabsf(bt.ny);
+                bt.fp = -cph_n;
+                bt.afp = fabsf(cph_n);
+                bt.efp = efp_n;
+            }
+            bt.pw = -(float)(pw0 + pw1);
+            bt.ang = -(float)(an0 + an1);
+            bt.aang = fabsf(bt.ang);
+            bt.eang = ea0n + ea1n;
+            bt.pwx = group_ballot<GL>(ea0n > 0.0f || ea1n > 0.0f, gbase) != 0 ? kPwEstU : 0;
+            float part[8], sm[8];
+            bound_parts(rm, n, c, nr, 0, bt, part);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            JW[k] = (uint32_t)__builtin_amdgcn_readlane((int)jw, k << 3);
-            JP[k + 1] = JP[k] + (int)(JW[k] >> 24) + __builtin_popcount((JW[k] >> 16) & 0xffu);
-        }
-        const Published<ObjP> Pall{&X0->P[0][0]};  // (every group's view, published above)
-        for (int q0 = 0; q0 < JP[K]; q0 += 64) {  // (wave-uniform trip count)
-            const int q = q0 + lane;
-            int G = 0, base = 0;
-            uint32_t w = JW[0];
+            for (int k = 0; k < 8; ++k) sm[k] = grp8_fsum(part[k]);
+            const Staged<float> B{SH->BS[K * hf + g]};
+            if (r == 0) {
 #pragma unroll
-            for (int k = 1; k < K; ++k) {
-                const bool ge = q >= JP[k];
-                G = ge ? k : G;
-                w = ge ? JW[k] : w;
-                base = ge ? JP[k] : base;
+                for (int k = 0; k < 8; ++k) B.put(k, sm[k]);
+                B.put(11, (float)bt.pwx);
             }
-            const int ql = q - base, nrtG = (int)(w >> 24);
-            const bool has = q < JP[K], isrel = ql < nrtG;
-            const int idx = nth_bit(isrel ? (w & 0xffffu) : ((w >> 16) & 0xffu), isrel ? ql : ql - nrtG);
-            const bool rel = has && isrel, foc = has && !isrel;
-            const ObjP* PG = Pall.ptr() + G * GL;
-            const RelConst& rc = Hd->rel[rel ? idx : 0];
-            const ObjP qo = PG[foc ? idx : 0];
-            double ay = 0.0, ax = 1.0, pw = 0.0;
-            float ti = 0.0f;
-            if (rel) pw = rel_pair(rc, PG, ay, ax, ti);
-            if (foc) {
-                ay = (double)(rm.fyf - qo.yf);
-                ax = (double)(rm.fxf - qo.xf);
-            }
-            const double at = atan2_ool(ay, ax);
-            const Staged<double> SG = Sall.at(G * S_W0);
-            if (rel) {
-                SG.put(S_PW + idx, -pw);
-                SG.put(S_ANG + idx, -rel_angle(rc, at, ti));
-            }
-            if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
-                const float b = (float)at - qo.rotYf;
-                SG.put(S_FP + idx, -(double)cos_f32((float)((double)b + kHalfPI)));
+            if (!exact_b) {  // the node's terms and their allowances, for its commit
+                if (r < n) {
+                    Sg.put(S_FP + r, -(double)cph_n);
+                    stage(Published<float>{X0->EO[g]}).put(r, efp_n);
+                }
+                if (r < nr) {
+                    Sg.put(S_PW + r, -pw0);
+                    Sg.put(S_ANG + r, -an0);
+                }
+                if (r + GL < nr) {
+                    Sg.put(S_PW + r + GL, -pw1);
+                    Sg.put(S_ANG + r + GL, -an1);
+                }
+                Sg.put(S_VBX + r, (double)ea0n);
+                Sg.put(S_VBY + r, (double)ea1n);
             }
         }
-        const Published<double> Sv = publish(Sall);
-        SSTAMP(3);
-        // The eight ordered sums: lane r of each group replays stream r (float sums round every
-        // partial sum to float; a double-rounded float add equals the float add, 53 >= 2*24+2),
-        // in the wavefront that built it (the list wavefront: 3, 4, 5); the workgroup barrier
-        // hands every node's to both chain wavefronts. The buffer alternates by batch.
+        SSTAMP(5);
         const Staged<double> SUMst{SH->SUM[par][K * hf + g]};
-        if (r <= 2 || r >= 6) {
-            int base = S_VBX, len = n;
-            bool rnd = true;
-            switch (r) {
-                case 0: base = S_VBX; len = n; rnd = true; break;
-                case 1: base = S_VBY; len = n; rnd = true; break;
-                case 2: base = S_FP; len = n; rnd = false; break;
-                case 6: base = S_PW; len = nr; rnd = false; break;
-                default: base = S_ANG; len = nr; rnd = false; break;
+        if (exact_b) {
+            // The exact FocalPoint terms of the group's moved objects and the terms of the
+            // relationships they touch (and of the carried terms that are estimates), the rest
+            // carried from the incoming state. The group's jobs (relationships first, then
+            // objects) are dealt out to its 8 lanes, one double atan2 per lane per pass
+            // (Kernel.cu:170-188, 222, 249-253, 271-277).
+            const bool fj = r < n && (moved || efp_c != 0.0f);
+            const bool t0j = t0 || (r < nr && ea0_c != 0.0f);
+            const bool t1j = t1 || (r + GL < nr && ea1_c != 0.0f);
+            const uint32_t fm = (uint32_t)group_ballot<GL>(fj, gbase);
+            const uint32_t tm = (uint32_t)group_ballot<GL>(t0j, gbase) |
+                                ((uint32_t)group_ballot<GL>(t1j, gbase) << GL);
+            const int nrt = __builtin_popcount(tm);
+            if (r < n) {
+                const float area = __int_as_float(Hd->objs[r].pad);
+                Sg.put(S_VBX + r, (double)area * sx);  // Kernel.cu:200-201
+                Sg.put(S_VBY + r, (double)area * sy);
+                if (!fj) Sg.put(S_FP + r, -(double)cph);
             }
-            const double* src = Sv.ptr() + g * S_W0 + base;
-            double acc = 0.0;
-            for (int l = 0; l < len; ++l) {
-                const double s = acc + src[l];
-                acc = rnd ? (double)(float)s : s;
+            if (r < nr && !t0j) {
+                Sg.put(S_PW + r, -rpw0);
+                Sg.put(S_ANG + r, -rang0);
             }
-            SUMst.put(r, acc);
+            if (r + GL < nr && !t1j) {
+                Sg.put(S_PW + r + GL, -rpw1);
+                Sg.put(S_ANG + r + GL, -rang1);
+            }
+            // The 8 nodes' jobs are dealt out to the wavefront's 64 lanes (one pass unless they
+            // number more than 64): lane q takes job q of the concatenation, group by group.
+            const uint32_t jw = tm | (fm << 16) | ((uint32_t)nrt << 24);  // (group-uniform)
+            uint32_t JW[K];
+            int JP[K + 1];
+            JP[0] = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                JW[k] = (uint32_t)__builtin_amdgcn_readlane((int)jw, k << 3);
+                JP[k + 1] = JP[k] + (int)(JW[k] >> 24) + __builtin_popcount((JW[k] >> 16) & 0xffu);
+            }
+            for (int q0 = 0; q0 < JP[K]; q0 += 64) {  // (wave-uniform trip count)
+                const int q = q0 + lane;
+                int G = 0, base = 0;
+                uint32_t w = JW[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    const bool ge = q >= JP[k];
+                    G = ge ? k : G;
+                    w = ge ? JW[k] : w;
+                    base = ge ? JP[k] : base;
+                }
+                const int ql = q - base, nrtG = (int)(w >> 24);
+                const bool has = q < JP[K], isrel = ql < nrtG;
+                const int idx = nth_bit(isrel ? (w & 0xffffu) : ((w >> 16) & 0xffu), isrel ? ql : ql - nrtG);
+                const bool rel = has && isrel, foc = has && !isrel;
+                const ObjP* PG = Pall.ptr() + G * GL;
+                const RelConst& rc = Hd->rel[rel ? idx : 0];
+                const ObjP qo = PG[foc ? idx : 0];
+                double ay = 0.0, ax = 1.0, pw = 0.0;
+                float ti = 0.0f;
+                if (rel) pw = rel_pair(rc, PG, ay, ax, ti);
+                if (foc) {
+                    ay = (double)(rm.fyf - qo.yf);
+                    ax = (double)(rm.fxf - qo.xf);
+                }
+                const double at = atan2_ool(ay, ax);
+                const Staged<double> SG = Sall.at(G * S_W0);
+                if (rel) {
+                    SG.put(S_PW + idx, -pw);
+                    SG.put(S_ANG + idx, -rel_angle(rc, at, ti));
+                }
+                if (foc) {  // focal_cos with the atan2 above (atan2_f32 rounds it once)
+                    const float b = (float)at - qo.rotYf;
+                    SG.put(S_FP + idx, -(double)cos_f32((float)((double)b + kHalfPI)));
+                }
+            }
+            const Published<double> Sv = publish(Sall);
+            SSTAMP(3);
+            // The eight ordered sums: lane r of each group replays stream r (float sums round
+            // every partial sum to float; a double-rounded float add equals the float add, 53 >=
+            // 2*24+2), in the wavefront that built it (the list wavefront: 3, 4, 5); the workgroup
+            // barrier hands every node's to both chain wavefronts. The buffer alternates by batch.
+            if (r <= 2 || r >= 6) {
+                int base = S_VBX, len = n;
+                bool rnd = true;
+                switch (r) {
+                    case 0: base = S_VBX; len = n; rnd = true; break;
+                    case 1: base = S_VBY; len = n; rnd = true; break;
+                    case 2: base = S_FP; len = n; rnd = false; break;
+                    case 6: base = S_PW; len = nr; rnd = false; break;
+                    default: base = S_ANG; len = nr; rnd = false; break;
+                }
+                const double* src = Sv.ptr() + g * S_W0 + base;
+                double acc = 0.0;
+                for (int l = 0; l < len; ++l) {
+                    const double s = acc + src[l];
+                    acc = rnd ? (double)(float)s : s;
+                }
+                SUMst.put(r, acc);
+            }
         }
         SSTAMP(4);
         const Published<double> SUMv = publish_workgroup(SUMst);
-        // (every half's streams were published by its chain wavefront before the same barrier;
-        // they are next rewritten after the next batch's views barrier)
+        // (every half's streams and bound sums were published by its wavefronts before the same
+        // barrier; they are next rewritten after the next batch's views barrier)
         auto streams_of = [&](int h) __attribute__((always_inline)) {
             return Published<double>{&X0of(h)->S[0][0]};
         };
+        const Published<float> BSv{&SH->BS[0][0]};
         par ^= 1;
         SSTAMP(6);
-        // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547), of node `lane`
-        // (lanes 0 .. NN-1; the others repeat node 0).
+        // Node `lane` (lanes 0 .. NN-1; the others repeat node 0).
         const int nd = lane < NN ? lane : 0;
+        // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
+        // total (the node whose configuration it started from, or the batch's incoming total).
+        const float u_dep = shfl_f(r_u, tr.dep < 64 ? tr.dep : 0);  // (record dep's uniform)
+        const float u_n = tr.dep < kb ? u_dep : 1.0f;
+        const int cpar_l = tr.cpar == kNone ? 0 : tr.cpar;
         float sc[8];
-        {
+        uint64_t ab = 0ull, ob = 0ull;  // accepted nodes; nodes the bound leaves open
+        float st_lo = 0.0f, st_hi = 0.0f;  // (bound batches) each node's total's interval
+        if (exact_b) {
+            // Costs(), Kernel.cu:518-549 (OffLimits never enters a step, :547)
             const double* sm = SUMv.ptr() + (nd - (K * hf + g)) * 8;  // (SUM[par][nd])
             const float nx = (float)sm[0], ny = (float)sm[1];
             const double fpd = sm[2];
@@ -876,23 +1074,82 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             t = t + sc[5];
             t = t + sc[7];
             sc[0] = t;
+            const float cp_tot = shfl_f(sc[0], cpar_l);
+            const float cur_n = tr.cpar == kNone ? cur[0] : cp_tot;
+            const bool acc_n = lane < NN && tr.dep < kb &&
+                               accept_u(u_n, kBeta * ((double)sc[0] - (double)cur_n));
+            ab = __ballot(acc_n);
         }
-        // Accept (Kernel.cu:706-713) at every node: its step's uniform against its current
-        // total (the node whose configuration it started from, or the batch's incoming total).
-        const float u_dep = shfl_f(r_u, tr.dep < 64 ? tr.dep : 0);  // (record dep's uniform)
-        const float u_n = tr.dep < kb ? u_dep : 1.0f;
-        const float cp_tot = shfl_f(sc[0], tr.cpar == kNone ? 0 : tr.cpar);
-        const float cur_n = tr.cpar == kNone ? cur[0] : cp_tot;
-        const bool acc_n = lane < NN && tr.dep < kb &&
-                           accept_u(u_n, kBeta * ((double)sc[0] - (double)cur_n));
-        const uint64_t ab = __ballot(acc_n);
+        if (bound_b) {
+            // the node's bound: its chain and list wavefronts' sums, composed (bound_te; the
+            // decision's arithmetic on the current total added per node, as bound_compose does)
+            const float* bs = BSv.ptr() + nd * kBS;
+            float sum[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sum[k] = bs[k] + (k >= 4 && k <= 6 ? bs[8 + (k - 4)] : 0.0f);
+            BoundTerms unused{};
+            float e0;
+            const float t = bound_te<false>(rm, n, nr, 8, (int)bs[11], sum, unused, CostIv{0.0f, 0.0f},
+                                            a.bound_slack, e0);
+            st_lo = t - 1.5f * e0;
+            st_hi = t + 1.5f * e0;
+            const float plo = shfl_f(st_lo, cpar_l), phi = shfl_f(st_hi, cpar_l);
+            CostIv cur_n = tr.cpar == kNone ? cur_iv : CostIv{plo, phi};
+#if MH_CHECK
+            // (check builds: against the exact current totals the exact decisions use)
+            {
+                const float pcx = shfl_f(sc[0], cpar_l);  // (every lane: an inactive source reads 0)
+                const float cx0 = tr.cpar == kNone ? cur[0] : pcx;
+                cur_n = CostIv{cx0, cx0};
+            }
+#endif
+            const float e = e0 + a.bound_slack * (3.0f * 0x1p-24f) *
+                                     fmaxf(fabsf(cur_n.lo), fabsf(cur_n.hi));
+            CostIv star;
+            const int d = bound_vs(t, e, u_n, cur_n, star);
+            const bool live = lane < NN && tr.dep < kb;
+#if MH_CHECK
+            if (live) {
+                const bool acc_x = ((ab >> lane) & 1ull) != 0;
+                MH_CK(st_lo != st_lo || (sc[0] >= st_lo && sc[0] <= st_hi), 22, __float_as_uint(sc[0]),
+                      __float_as_uint(st_hi - st_lo));
+                MH_CK(d != BOUND_REJECT || !acc_x, 20, __float_as_uint(sc[0]), __float_as_uint(t));
+                MH_CK(d != BOUND_ACCEPT || acc_x, 21, __float_as_uint(sc[0]), __float_as_uint(t));
+                if ((d == BOUND_REJECT && acc_x) || (d == BOUND_ACCEPT && !acc_x)) {
+                    if (atomicCAS(&g_spec_ck[0], 0u, 1u) == 0u) {  // (the first one's inputs)
+                        g_spec_ck[1] = __float_as_uint(sc[0]);
+                        g_spec_ck[2] = __float_as_uint(t);
+                        g_spec_ck[3] = __float_as_uint(e);
+                        g_spec_ck[4] = __float_as_uint(cur_n.lo);
+                        g_spec_ck[5] = __float_as_uint(u_n);
+                        g_spec_ck[6] = (unsigned)d | ((unsigned)lane << 8) | ((unsigned)tr.dep << 16);
+                        g_spec_ck[7] = (unsigned)tr.cpar | ((unsigned)kb << 8) | ((unsigned)H << 16);
+                        g_spec_ck[8] = __float_as_uint(cur[0]);
+                        g_spec_ck[9] = (unsigned)done;
+                        g_spec_ck[10] = __float_as_uint(e0);
+                        g_spec_ck[11] = (unsigned)hf;
+                    }
+                }
+                mh_count_decision(d, true);
+                atomicAdd(&g_check[5], 1u);
+            }
+#else
+            ab = __ballot(live && d == BOUND_ACCEPT);
+            ob = __ballot(live && d == BOUND_OPEN);
+#endif
+        }
         // The realised path from the root: its nodes' steps commit; the configuration after
-        // them is the last accepted node's (or the incoming one).
+        // them is the last accepted node's (or the incoming one). A node the bound leaves open
+        // ends the path before its step, which the next batch evaluates exactly.
         int node = 0, steps = 0, last = kNone, nacc = 0;
         unsigned int acc_steps = 0;
 #pragma unroll
         for (int d = 0; d < NN; ++d) {
             if (node == kNone || d >= kb) break;
+            if ((ob >> node) & 1ull) {
+                exact_next = true;
+                break;
+            }
             ++steps;
             const bool an = ((ab >> node) & 1ull) != 0;
             if (an) {
@@ -901,6 +1158,26 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                 acc_steps |= 1u << d;
             }
             node = __builtin_amdgcn_readlane(an ? tr.cha : tr.chr, node);
+        }
+        if (exact_b) exact_next = !BOUND;
+        if (refresh) {
+            // node 0 evaluated the incoming configuration: its exact costs and terms are the
+            // current ones
+            const double* sl = streams_of(0).ptr();
+            if (r < n) cph = (float)(-sl[S_FP + r]);
+            if (r < nr) {
+                rpw0 = -sl[S_PW + r];
+                rang0 = -sl[S_ANG + r];
+            }
+            if (r + GL < nr) {
+                rpw1 = -sl[S_PW + r + GL];
+                rang1 = -sl[S_ANG + r + GL];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], 0);
+            cur_iv = CostIv{cur[0], cur[0]};
+            cur_exact = true;
+            efp_c = ea0_c = ea1_c = 0.0f;
         }
         if (last != kNone) {
             const int lh = last / K, lg = last % K;
@@ -925,8 +1202,19 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                 rpw1 = -sl[S_PW + r + GL];
                 rang1 = -sl[S_ANG + r + GL];
             }
+            if (exact_b) {  // (every term of an exact batch's node is exact)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last);
+                for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], last);
+                cur_iv = CostIv{cur[0], cur[0]};
+                cur_exact = true;
+                efp_c = ea0_c = ea1_c = 0.0f;
+            } else {
+                cur_iv = CostIv{readlane_f(st_lo, last), readlane_f(st_hi, last)};
+                cur_exact = false;
+                efp_c = r < n ? X0of(lh)->EO[lg][r] : 0.0f;
+                ea0_c = (float)sl[S_VBX + r];
+                ea1_c = (float)sl[S_VBY + r];
+            }
             accepted += (unsigned int)nacc;
             // An accepted swap also exchanges z, rotX and rotZ (:675-700), object 1's values
             // through float temporaries, in step order (a later swap sees an earlier one's).
@@ -960,8 +1248,8 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                 g_spec_dbg[base + 3] = prod_seen;
                 g_spec_dbg[base + 4] = (unsigned)last;
                 g_spec_dbg[base + 5] = (unsigned)steps;
-                g_spec_dbg[base + 6] = __float_as_uint(cur[0]);
-                g_spec_dbg[base + 7] = (unsigned)nacc;
+                g_spec_dbg[base + 6] = __float_as_uint(cur_iv.lo);
+                g_spec_dbg[base + 7] = (unsigned)nacc | (exact_b ? 0x100u : 0u) | (refresh ? 0x200u : 0u);
                 g_spec_dbg_n = base + 8;
             }
         }
@@ -981,6 +1269,8 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
 #if MH_STAMPS
         cyc[14] += 1;
         cyc[15] += (unsigned long long)steps;
+        cyc[13] += exact_b ? 1 : 0;
+        cyc[12] += refresh ? 1 : 0;
 #endif
     }
 #if MH_STAMPS
@@ -1044,24 +1334,52 @@ int spec_waves_per_chain(int halves) { return 2 * (halves >= 2 ? 2 : 1); }
 // Whether the speculative kernel serves a room: at most GL objects, RMAX relationships.
 bool spec_fits(int n, int c, int r) { return n >= 1 && n <= GL && c <= GL && r <= RMAX; }
 
-int spec_blocks_per_cu(int halves) {
+template <int H, bool B>
+int spec_blocks_of() {
     int blocks = 0;
-    const hipError_t e =
-        halves >= 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel<2>, 256,
-                                                                   spec_lds_bytes(2))
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel<1>, 128,
-                                                                   spec_lds_bytes(1));
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_spec_kernel<H, B>,
+                                                                       128 * H, spec_lds_bytes(H));
     return e == hipSuccess ? blocks : 0;
+}
+
+int spec_blocks_per_cu(int halves, bool bound) {
+    if (halves >= 2) return bound ? spec_blocks_of<2, true>() : spec_blocks_of<2, false>();
+    return bound ? spec_blocks_of<1, true>() : spec_blocks_of<1, false>();
+}
+
+// The instance: halves, and decisions on the bound (a.spec_bound) or on exact costs alone.
+template <int H, bool B>
+void launch_spec_of(const LaunchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((mh_spec_kernel<H, B>), dim3((unsigned)a.n_chains), dim3(128 * H),
+                       spec_lds_bytes(H), s, a);  // (one chain per workgroup)
 }
 
 hipError_t launch_spec(const LaunchArgs& a, int halves, hipStream_t s) {
     if (a.n_chains <= 0) return hipSuccess;
-    const dim3 grid((unsigned)a.n_chains);  // one chain per workgroup
-    if (halves >= 2)
-        hipLaunchKernelGGL(mh_spec_kernel<2>, grid, dim3(256), spec_lds_bytes(2), s, a);
-    else
-        hipLaunchKernelGGL(mh_spec_kernel<1>, grid, dim3(128), spec_lds_bytes(1), s, a);
+    if (halves >= 2) {
+        if (a.spec_bound) launch_spec_of<2, true>(a, s);
+        else launch_spec_of<2, false>(a, s);
+    } else {
+        if (a.spec_bound) launch_spec_of<1, true>(a, s);
+        else launch_spec_of<1, false>(a, s);
+    }
     return hipGetLastError();
 }
 
 }  // namespace mh
+
+#if MH_CHECK
+extern "C" __attribute__((visibility("default"))) int mh_debug_spec_ck(unsigned int* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_ck), sizeof(unsigned int) * 12) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int mh_debug_check_spec(unsigned int* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check), sizeof(unsigned int) * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int mh_debug_decisions_spec(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decide), sizeof(unsigned long long) * 4) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif

@@ -41,7 +41,13 @@ CASES = [("syn", 64, 8192, 2000, "full"), ("syn", 256, 2048, 1500, "incremental"
          ("wild", 64, 1024, 1000, "full"), ("wild", 256, 512, 500, "incremental"),
          # the round-5 download fault's test shape (test_bound_decision_paths[main-32]): the
          # console harness's room, current costs read, then the final pass (index-checked)
-         ("main", 32, 512, 600, "full"), ("main", 32, 512, 600, "incremental")]
+         ("main", 32, 512, 600, "full"), ("main", 32, 512, 600, "incremental"),
+         # the speculative kernel's instance that decides on the bound (mh_spec.hip: nodes'
+         # bounds against their exact costs, at every node of every batch): config 2's room, a
+         # wrapped one, negated weights, poses far outside the symmetry range; 16- and 8-node trees
+         ("syn", 8, 256, 3000, "speculative"), ("syn", 8, 1024, 3000, "speculative-h1"),
+         ("wrap", 8, 512, 2000, "speculative"), ("negw", 8, 512, 2000, "speculative"),
+         ("wild", 8, 256, 1000, "speculative")]
 
 
 def room_of(mh, kind, n):
@@ -69,7 +75,10 @@ def one(kind, n, chains, steps, kernel):
     import __graft_entry__ as graft
     mh = graft.load_package()
     os.environ["MH_DELTA"] = "1" if kernel == "incremental" else "0"
-    os.environ["MH_SPEC"] = "0"  # (the speculative kernel takes no decision on the bound)
+    os.environ["MH_SPEC"] = "1" if kernel.startswith("speculative") else "0"
+    os.environ["MH_SPEC_BOUND"] = "1"
+    os.environ["MH_SPEC_H"] = "1" if kernel.endswith("-h1") else ""
+    kernel = kernel.split("-")[0]
     lib = mh.load_library(str(LIB))
     mh.abi._lib = lib  # the Session wrapper uses the module's library
     room = room_of(mh, kind, n)
@@ -80,21 +89,33 @@ def one(kind, n, chains, steps, kernel):
         s.finalize()
         _, costs = s.download()
     ck = (C.c_uint * 8)()
-    fn = lib.mh_debug_check_delta if kernel == "incremental" else lib.mh_debug_check
+    fn = {"incremental": lib.mh_debug_check_delta,
+          "speculative": lib.mh_debug_check_spec}.get(kernel, lib.mh_debug_check)
     assert fn(ck) == 0
-    if kernel == "incremental":  # (the init and final passes are the full kernel's: its record)
+    if kernel != "full":  # (the init and final passes are the full kernel's: its record)
         ckf = (C.c_uint * 8)()
         assert lib.mh_debug_check(ckf) == 0
         if ckf[0] and not ck[0]:
             ck[0], ck[1], ck[2], ck[3] = ckf[0], ckf[1], ckf[2], ckf[3]
+    if kernel == "speculative" and ck[0]:
+        import struct
+        g = (C.c_uint * 12)()
+        assert lib.mh_debug_spec_ck(g) == 0
+        f = lambda v: struct.unpack("f", struct.pack("I", v))[0]
+        print(f"[spec-ck] sc={f(g[1])!r} t={f(g[2])!r} e={f(g[3])!r} cur={f(g[4])!r} u={f(g[5])!r} "
+              f"d={g[6] & 255} node={(g[6] >> 8) & 255} dep={g[6] >> 16} cpar={g[7] & 255} "
+              f"kb={(g[7] >> 8) & 255} H={g[7] >> 16} cur0={f(g[8])!r} done={g[9]} e0={f(g[10])!r} "
+              f"hf={g[11]}", flush=True)
     dc = (C.c_ulonglong * 4)()
-    fd = lib.mh_debug_decisions_delta if kernel == "incremental" else lib.mh_debug_decisions
+    fd = {"incremental": lib.mh_debug_decisions_delta,
+          "speculative": lib.mh_debug_decisions_spec}.get(kernel, lib.mh_debug_decisions)
     assert fd(dc) == 0
     steps_all = float(chains * steps)
     rates = (f"; of {chains * steps} steps: certain reject {dc[1] / steps_all:.4f}, certain "
              f"accept {dc[2] / steps_all:.4f}, open {(dc[0] - dc[1] - dc[2]) / steps_all:.4f}, "
              f"exact current pass {dc[3] / steps_all:.4f}") if dc[0] else ""
     site = SITES.get(ck[1], str(ck[1]))
+    # (speculative: decisions at every evaluated node, the realised path's and the others')
     print(f"[bound] {kind} N={n} {kernel}: {chains} x {steps} steps, {ck[5]} bound decisions "
           f"checked, violations {ck[0]}" + (f" (first: {site}, values {ck[2]:#x} {ck[3]:#x})"
                                             if ck[0] else "") + rates, flush=True)

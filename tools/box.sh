@@ -15,6 +15,7 @@
 #                        others abvar/libmhgpu_<v>.so), $MH_AB_REPS alternations
 #   prof=N,chains,iters,steps    tools/profile_box.sh: kernel trace + the PMC passes
 #   bound                tools/bound_check.py (every room, full length)
+#   bound=<room>,N,chains,steps,kernel[;...]   those cases only
 #   stamps=N,chains,iters        tools/stamps.py on abvar/libmhgpu_stamps.so
 #   spread=N,chains,launches,iters  tools/launch_spread.py (per-launch time and bound decisions)
 # Example:
@@ -59,9 +60,15 @@ for STEP in "$@"; do
       set -- ${VAL//,/ }
       bash tools/profile_box.sh "$TAG/prof_n$1" --objects $1 --chains $2 --iters $3 --steps $4 \
           --warmup 1 --no-cpu-baseline --e2e-iters 0 || exit 1 ;;
-    bound)
-      timeout -k 10 1000 python -u tools/bound_check.py > "$OUT/bound.txt" 2>&1
-      rc=$?; grep "\[bound\]" "$OUT/bound.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    bound)  # (bound=<room>,N,chains,steps,kernel[;...]: those cases only)
+      if [ -z "$VAL" ]; then
+        timeout -k 10 1000 python -u tools/bound_check.py > "$OUT/bound.txt" 2>&1
+      else
+        for CASE in ${VAL//;/ }; do
+          timeout -k 10 300 python -u tools/bound_check.py --one ${CASE//,/ } >> "$OUT/bound.txt" 2>&1 || break
+        done
+      fi
+      rc=$?; grep "\[bound\]" "$OUT/bound.txt"; [ $rc -eq 0 ] || { tail -20 "$OUT/bound.txt"; exit $rc; } ;;
     stamps)
       set -- ${VAL//,/ }
       MH_LIB=abvar/libmhgpu_stamps.so timeout -k 10 300 python tools/stamps.py $1 $2 $3 \

@@ -6,6 +6,7 @@ Read the SHARES, not the absolute time: the stamps' waits forbid some overlap.""
 import ctypes as C
 import os
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -16,7 +17,8 @@ import __graft_entry__ as graft  # noqa: E402
 DELTA_PHASES = ["propose+objects", "clearance delta", "relationships", "symmetry delta",
                 "bound + term lists", "replay", "accept/restore", "(replay: dense part)"]
 SPEC_PHASES = ["tree + record count", "apply", "views barrier (wait for wave 1)",
-               "jobs (exact terms)", "own ordered sums", "", "sums barrier (wait for wave 1)",
+               "jobs (exact terms)", "own ordered sums", "bound (estimates, parts)",
+               "sums barrier (wait for wave 1)",
                "costs + accept + commit", "", "", "", ""]
 PHASES = ["propose", "A per-object", "B symmetry", "C clearance pairs", "D reject bound",
           "E SA walk + CL list", "F PW/ANG + replay", "accept/undo"]
@@ -32,8 +34,13 @@ def main():
         lanes, cpw, s_kind = s.step_kernel()
         print(f"[stamps] session created: {lanes} lanes/chain, {cpw} chains/workgroup, {s_kind}",
               flush=True)
+        s.run(0)
+        s.current_costs()  # (synchronises the set-up)
+        t0 = time.perf_counter()
         s.run(iters)
-        print("[stamps] run launched", flush=True)
+        s.current_costs()  # (synchronises)
+        wall = time.perf_counter() - t0
+        print(f"[stamps] run: {wall * 1e3:.3f} ms wall for {iters} steps", flush=True)
         s.finalize()
         print("[stamps] finalize launched", flush=True)
         acc_rate = s.summary().accepted / float(chains * iters)
@@ -43,12 +50,15 @@ def main():
         print(f"[check] violations={ck[0]} first site={ck[1]} values=({ck[2]}, {ck[3]}) "
               f"wave={ck[4]}", flush=True)
     out = (C.c_ulonglong * 16)()
+    if not hasattr(lib, "mh_debug_phase_cycles"):  # (a library without stamps: the wall time only)
+        return
     if s_kind == "speculative":  # one chain per wavefront, per-batch phases
         assert lib.mh_debug_spec_cycles(out) == 0
-        tot = sum(out[:12])
+        tot = sum(out[:12])  # ([12] refresh batches, [13] exact batches, [14], [15] counts)
         batches, steps = out[14], out[15]
         print(f"N={n} chains={chains} iters={iters} speculative acceptance={acc_rate:.4f} "
-              f"steps per batch {steps / max(1, batches):.3f}")
+              f"steps per batch {steps / max(1, batches):.3f}; batches: {batches} "
+              f"(exact {out[13]}, of them refresh {out[12]})")
         for name, v in zip(SPEC_PHASES, out[:12]):
             if not name:
                 continue
