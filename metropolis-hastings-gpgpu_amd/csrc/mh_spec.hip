@@ -572,50 +572,52 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                     Sst.put(S_SYM + r, -(double)sym_row(Pg, pv.b.ptr(), n, rxr, ryr, rr, exact_mode));
             }
             const auto sv = publish(Sst, CLBst);
-            if (bound_b) {
-                // The node's bound, this wavefront's share (bound_parts): the row maximum's fp32
-                // estimate with sym_err's allowance (max(0, .) is 1-Lipschitz, and the exact row
-                // maximum lies within the estimate's allowance of the largest estimate), the
-                // lane's column of Clearance terms in clearance order, its SurfaceArea terms.
-                BoundTerms bt{};
-                bt.k = 8;
-                if (r < n) {
-                    float m1 = -INFINITY;
-                    for (int j = 0; j < n; ++j)
-                        m1 = fmaxf(m1, sym_val_fast(objp_f4(Pg[j]), rxr, ryr, rr));
-                    const float mx = fmaxf(0.0f, m1);
-                    bt.esym = sym_err(m1, rr);
-                    bt.sym = -mx;
-                    bt.symw = (float)(n - r) * (mx + bt.esym);  // (row r: position r)
-                    float cls = 0.0f;
-                    for (int i = 0; i < c; ++i) {
-                        const float ov = overlap(sv.b[i], box);
-                        cls += ov;
-                        bt.kcl += ov != 0.0f ? 1 : 0;
+            if constexpr (BOUND || MH_CHECK) {  // (the exact instance compiles none of it)
+                if (bound_b) {
+                    // The node's bound, this wavefront's share (bound_parts): the row maximum's fp32
+                    // estimate with sym_err's allowance (max(0, .) is 1-Lipschitz, and the exact row
+                    // maximum lies within the estimate's allowance of the largest estimate), the
+                    // lane's column of Clearance terms in clearance order, its SurfaceArea terms.
+                    BoundTerms bt{};
+                    bt.k = 8;
+                    if (r < n) {
+                        float m1 = -INFINITY;
+                        for (int j = 0; j < n; ++j)
+                            m1 = fmaxf(m1, sym_val_fast(objp_f4(Pg[j]), rxr, ryr, rr));
+                        const float mx = fmaxf(0.0f, m1);
+                        bt.esym = sym_err(m1, rr);
+                        bt.sym = -mx;
+                        bt.symw = (float)(n - r) * (mx + bt.esym);  // (row r: position r)
+                        float cls = 0.0f;
+                        for (int i = 0; i < c; ++i) {
+                            const float ov = overlap(sv.b[i], box);
+                            cls += ov;
+                            bt.kcl += ov != 0.0f ? 1 : 0;
+                        }
+                        bt.cl = -cls;
                     }
-                    bt.cl = -cls;
+                    bt.sa = -((sac.x + sac.y + sac.z + sac.w) + (sao.x + sao.y + sao.z + sao.w));
+                    int ncl = bt.kcl;  // (the node's non-zero Clearance terms)
+                    ncl += __builtin_amdgcn_update_dpp(0, ncl, 0xB1, 0xF, 0xF, false);
+                    ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x4E, 0xF, 0xF, false);
+                    ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x141, 0xF, 0xF, false);
+                    float part[8];
+                    bound_parts(rm, n, c, nr, ncl, bt, part);
+                    // a pose outside the range the symmetry estimate is proven for: no bound (NaN)
+                    const float lin = exact_mode ? __builtin_nanf("") : part[4];
+                    const float s4 = grp8_fsum(lin), s5 = grp8_fsum(part[5]), s6 = grp8_fsum(part[6]);
+                    const Staged<float> B{SH->BS[K * hf + g]};
+                    if (r == 0) {
+                        B.put(8, s4);
+                        B.put(9, s5);
+                        B.put(10, s6);
+                    }
                 }
-                bt.sa = -((sac.x + sac.y + sac.z + sac.w) + (sao.x + sao.y + sao.z + sao.w));
-                int ncl = bt.kcl;  // (the node's non-zero Clearance terms)
-                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0xB1, 0xF, 0xF, false);
-                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x4E, 0xF, 0xF, false);
-                ncl += __builtin_amdgcn_update_dpp(0, ncl, 0x141, 0xF, 0xF, false);
-                float part[8];
-                bound_parts(rm, n, c, nr, ncl, bt, part);
-                // a pose outside the range the symmetry estimate is proven for: no bound (NaN)
-                const float lin = exact_mode ? __builtin_nanf("") : part[4];
-                const float s4 = grp8_fsum(lin), s5 = grp8_fsum(part[5]), s6 = grp8_fsum(part[6]);
-                const Staged<float> B{SH->BS[K * hf + g]};
-                if (r == 0) {
-                    B.put(8, s4);
-                    B.put(9, s5);
-                    B.put(10, s6);
+                if (!exact_b) {  // (the barrier below publishes the bound's sums)
+                    publish_workgroup(Staged<double>{SH->SUM[par][K * hf + g]});
+                    par ^= 1;
+                    continue;
                 }
-            }
-            if (!exact_b) {  // (the barrier below publishes the bound's sums)
-                publish_workgroup(Staged<double>{SH->SUM[par][K * hf + g]});
-                par ^= 1;
-                continue;
             }
             // The non-zero Clearance terms, clearance-major (:408-431), and SurfaceArea terms
             // (clearances, then objects, :445-480), compacted in the reference's order.
@@ -854,82 +856,84 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             t1 = (((mv >> rc.s) | (mv >> rc.t) | (mv >> rc.as) | (mv >> rc.at)) & 1u) != 0;
         }
         const Staged<double> Sg = Sall.at(g * S_W0);
-        if (bound_b) {
-            // The node's bound, this wavefront's share: the VisualBalance products, the moved
-            // objects' FocalPoint terms and the touched relationships' terms as fp32 estimates
-            // (exact where an estimate cannot vouch for its branch), the rest carried.
-            float cph_n = cph, efp_n = efp_c;
-            double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
-            float ea0n = ea0_c, ea1n = ea1_c;
-            const ObjP* PGg = Pall.ptr() + g * GL;
-            if (moved && r < n) {
-                ObjP p;
-                p.xf = xf;
-                p.yf = yf;
-                p.rotYf = ryf;
-                p.pad = 0.0f;
-                const float fy = rm.fyf - yf, fx = rm.fxf - xf;
-                bool ambo = !(fmaxf(fabsf(fy), fabsf(fx)) >= 0x1p-100f);
-                cph_n = cph_est(atan2_est(fy, fx), p, ambo);
-                efp_n = kDeltaCph;
-                if (ambo) cph_n = __builtin_nanf("");  // (an invalid bound: the node is open)
-            }
-            auto rel_est = [&](int q, double& pw, double& an, float& ea) __attribute__((always_inline)) {
-                const RelConst& rc = Hd->rel[q];
-                const float4 e0 = Hd->re0[q], e1 = Hd->re1[q];
-                bool amb = false;
-                pw = rel_pw_est(e0, PGg[rc.s], PGg[rc.t], amb);
-                const ObjP as = PGg[rc.as], atp = PGg[rc.at];
-                const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
-                amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
-                an = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
-                if (amb) pw = __builtin_nan("");  // (an estimate that cannot vouch for its branch:
-                                                  // the node is open, its exact terms next batch)
-            };
-            if (t0) rel_est(r, pw0, an0, ea0n);
-            if (t1) rel_est(r + GL, pw1, an1, ea1n);
-            BoundTerms bt{};
-            bt.k = 8;
-            if (r < n) {
-                const float area = __int_as_float(Hd->objs[r].pad);
-                bt.nx = (float)((double)area * sx);  // Kernel.cu:200-201
-                bt.ny = (float)((double)area * sy);
-                bt.anx = fabsf(bt.nx);
-                bt.any = fabsf(bt.ny);
-                bt.fp = -cph_n;
-                bt.afp = fabsf(cph_n);
-                bt.efp = efp_n;
-            }
-            bt.pw = -(float)(pw0 + pw1);
-            bt.ang = -(float)(an0 + an1);
-            bt.aang = fabsf(bt.ang);
-            bt.eang = ea0n + ea1n;
-            bt.pwx = group_ballot<GL>(ea0n > 0.0f || ea1n > 0.0f, gbase) != 0 ? kPwEstU : 0;
-            float part[8], sm[8];
-            bound_parts(rm, n, c, nr, 0, bt, part);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) sm[k] = grp8_fsum(part[k]);
-            const Staged<float> B{SH->BS[K * hf + g]};
-            if (r == 0) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) B.put(k, sm[k]);
-                B.put(11, (float)bt.pwx);
-            }
-            if (!exact_b) {  // the node's terms and their allowances, for its commit
+        if constexpr (BOUND || MH_CHECK) {  // (the exact instance compiles none of it)
+            if (bound_b) {
+                // The node's bound, this wavefront's share: the VisualBalance products, the moved
+                // objects' FocalPoint terms and the touched relationships' terms as fp32 estimates
+                // (exact where an estimate cannot vouch for its branch), the rest carried.
+                float cph_n = cph, efp_n = efp_c;
+                double pw0 = rpw0, an0 = rang0, pw1 = rpw1, an1 = rang1;
+                float ea0n = ea0_c, ea1n = ea1_c;
+                const ObjP* PGg = Pall.ptr() + g * GL;
+                if (moved && r < n) {
+                    ObjP p;
+                    p.xf = xf;
+                    p.yf = yf;
+                    p.rotYf = ryf;
+                    p.pad = 0.0f;
+                    const float fy = rm.fyf - yf, fx = rm.fxf - xf;
+                    bool ambo = !(fmaxf(fabsf(fy), fabsf(fx)) >= 0x1p-100f);
+                    cph_n = cph_est(atan2_est(fy, fx), p, ambo);
+                    efp_n = kDeltaCph;
+                    if (ambo) cph_n = __builtin_nanf("");  // (an invalid bound: the node is open)
+                }
+                auto rel_est = [&](int q, double& pw, double& an, float& ea) __attribute__((always_inline)) {
+                    const RelConst& rc = Hd->rel[q];
+                    const float4 e0 = Hd->re0[q], e1 = Hd->re1[q];
+                    bool amb = false;
+                    pw = rel_pw_est(e0, PGg[rc.s], PGg[rc.t], amb);
+                    const ObjP as = PGg[rc.as], atp = PGg[rc.at];
+                    const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
+                    amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
+                    an = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
+                    if (amb) pw = __builtin_nan("");  // (an estimate that cannot vouch for its branch:
+                                                      // the node is open, its exact terms next batch)
+                };
+                if (t0) rel_est(r, pw0, an0, ea0n);
+                if (t1) rel_est(r + GL, pw1, an1, ea1n);
+                BoundTerms bt{};
+                bt.k = 8;
                 if (r < n) {
-                    Sg.put(S_FP + r, -(double)cph_n);
-                    stage(Published<float>{X0->EO[g]}).put(r, efp_n);
+                    const float area = __int_as_float(Hd->objs[r].pad);
+                    bt.nx = (float)((double)area * sx);  // Kernel.cu:200-201
+                    bt.ny = (float)((double)area * sy);
+                    bt.anx = fabsf(bt.nx);
+                    bt.any = fabsf(bt.ny);
+                    bt.fp = -cph_n;
+                    bt.afp = fabsf(cph_n);
+                    bt.efp = efp_n;
                 }
-                if (r < nr) {
-                    Sg.put(S_PW + r, -pw0);
-                    Sg.put(S_ANG + r, -an0);
+                bt.pw = -(float)(pw0 + pw1);
+                bt.ang = -(float)(an0 + an1);
+                bt.aang = fabsf(bt.ang);
+                bt.eang = ea0n + ea1n;
+                bt.pwx = group_ballot<GL>(ea0n > 0.0f || ea1n > 0.0f, gbase) != 0 ? kPwEstU : 0;
+                float part[8], sm[8];
+                bound_parts(rm, n, c, nr, 0, bt, part);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sm[k] = grp8_fsum(part[k]);
+                const Staged<float> B{SH->BS[K * hf + g]};
+                if (r == 0) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) B.put(k, sm[k]);
+                    B.put(11, (float)bt.pwx);
                 }
-                if (r + GL < nr) {
-                    Sg.put(S_PW + r + GL, -pw1);
-                    Sg.put(S_ANG + r + GL, -an1);
+                if (!exact_b) {  // the node's terms and their allowances, for its commit
+                    if (r < n) {
+                        Sg.put(S_FP + r, -(double)cph_n);
+                        stage(Published<float>{X0->EO[g]}).put(r, efp_n);
+                    }
+                    if (r < nr) {
+                        Sg.put(S_PW + r, -pw0);
+                        Sg.put(S_ANG + r, -an0);
+                    }
+                    if (r + GL < nr) {
+                        Sg.put(S_PW + r + GL, -pw1);
+                        Sg.put(S_ANG + r + GL, -an1);
+                    }
+                    Sg.put(S_VBX + r, (double)ea0n);
+                    Sg.put(S_VBY + r, (double)ea1n);
                 }
-                Sg.put(S_VBX + r, (double)ea0n);
-                Sg.put(S_VBY + r, (double)ea1n);
             }
         }
         SSTAMP(5);
@@ -1080,63 +1084,65 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                                accept_u(u_n, kBeta * ((double)sc[0] - (double)cur_n));
             ab = __ballot(acc_n);
         }
-        if (bound_b) {
-            // the node's bound: its chain and list wavefronts' sums, composed (bound_te; the
-            // decision's arithmetic on the current total added per node, as bound_compose does)
-            const float* bs = BSv.ptr() + nd * kBS;
-            float sum[8];
+        if constexpr (BOUND || MH_CHECK) {  // (the exact instance compiles none of it)
+            if (bound_b) {
+                // the node's bound: its chain and list wavefronts' sums, composed (bound_te; the
+                // decision's arithmetic on the current total added per node, as bound_compose does)
+                const float* bs = BSv.ptr() + nd * kBS;
+                float sum[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) sum[k] = bs[k] + (k >= 4 && k <= 6 ? bs[8 + (k - 4)] : 0.0f);
-            BoundTerms unused{};
-            float e0;
-            const float t = bound_te<false>(rm, n, nr, 8, (int)bs[11], sum, unused, CostIv{0.0f, 0.0f},
-                                            a.bound_slack, e0);
-            st_lo = t - 1.5f * e0;
-            st_hi = t + 1.5f * e0;
-            const float plo = shfl_f(st_lo, cpar_l), phi = shfl_f(st_hi, cpar_l);
-            CostIv cur_n = tr.cpar == kNone ? cur_iv : CostIv{plo, phi};
+                for (int k = 0; k < 8; ++k) sum[k] = bs[k] + (k >= 4 && k <= 6 ? bs[8 + (k - 4)] : 0.0f);
+                BoundTerms unused{};
+                float e0;
+                const float t = bound_te<false>(rm, n, nr, 8, (int)bs[11], sum, unused, CostIv{0.0f, 0.0f},
+                                                a.bound_slack, e0);
+                st_lo = t - 1.5f * e0;
+                st_hi = t + 1.5f * e0;
+                const float plo = shfl_f(st_lo, cpar_l), phi = shfl_f(st_hi, cpar_l);
+                CostIv cur_n = tr.cpar == kNone ? cur_iv : CostIv{plo, phi};
 #if MH_CHECK
-            // (check builds: against the exact current totals the exact decisions use)
-            {
-                const float pcx = shfl_f(sc[0], cpar_l);  // (every lane: an inactive source reads 0)
-                const float cx0 = tr.cpar == kNone ? cur[0] : pcx;
-                cur_n = CostIv{cx0, cx0};
-            }
-#endif
-            const float e = e0 + a.bound_slack * (3.0f * 0x1p-24f) *
-                                     fmaxf(fabsf(cur_n.lo), fabsf(cur_n.hi));
-            CostIv star;
-            const int d = bound_vs(t, e, u_n, cur_n, star);
-            const bool live = lane < NN && tr.dep < kb;
-#if MH_CHECK
-            if (live) {
-                const bool acc_x = ((ab >> lane) & 1ull) != 0;
-                MH_CK(st_lo != st_lo || (sc[0] >= st_lo && sc[0] <= st_hi), 22, __float_as_uint(sc[0]),
-                      __float_as_uint(st_hi - st_lo));
-                MH_CK(d != BOUND_REJECT || !acc_x, 20, __float_as_uint(sc[0]), __float_as_uint(t));
-                MH_CK(d != BOUND_ACCEPT || acc_x, 21, __float_as_uint(sc[0]), __float_as_uint(t));
-                if ((d == BOUND_REJECT && acc_x) || (d == BOUND_ACCEPT && !acc_x)) {
-                    if (atomicCAS(&g_spec_ck[0], 0u, 1u) == 0u) {  // (the first one's inputs)
-                        g_spec_ck[1] = __float_as_uint(sc[0]);
-                        g_spec_ck[2] = __float_as_uint(t);
-                        g_spec_ck[3] = __float_as_uint(e);
-                        g_spec_ck[4] = __float_as_uint(cur_n.lo);
-                        g_spec_ck[5] = __float_as_uint(u_n);
-                        g_spec_ck[6] = (unsigned)d | ((unsigned)lane << 8) | ((unsigned)tr.dep << 16);
-                        g_spec_ck[7] = (unsigned)tr.cpar | ((unsigned)kb << 8) | ((unsigned)H << 16);
-                        g_spec_ck[8] = __float_as_uint(cur[0]);
-                        g_spec_ck[9] = (unsigned)done;
-                        g_spec_ck[10] = __float_as_uint(e0);
-                        g_spec_ck[11] = (unsigned)hf;
-                    }
+                // (check builds: against the exact current totals the exact decisions use)
+                {
+                    const float pcx = shfl_f(sc[0], cpar_l);  // (every lane: an inactive source reads 0)
+                    const float cx0 = tr.cpar == kNone ? cur[0] : pcx;
+                    cur_n = CostIv{cx0, cx0};
                 }
-                mh_count_decision(d, true);
-                atomicAdd(&g_check[5], 1u);
-            }
-#else
-            ab = __ballot(live && d == BOUND_ACCEPT);
-            ob = __ballot(live && d == BOUND_OPEN);
 #endif
+                const float e = e0 + a.bound_slack * (3.0f * 0x1p-24f) *
+                                         fmaxf(fabsf(cur_n.lo), fabsf(cur_n.hi));
+                CostIv star;
+                const int d = bound_vs(t, e, u_n, cur_n, star);
+                const bool live = lane < NN && tr.dep < kb;
+#if MH_CHECK
+                if (live) {
+                    const bool acc_x = ((ab >> lane) & 1ull) != 0;
+                    MH_CK(st_lo != st_lo || (sc[0] >= st_lo && sc[0] <= st_hi), 22, __float_as_uint(sc[0]),
+                          __float_as_uint(st_hi - st_lo));
+                    MH_CK(d != BOUND_REJECT || !acc_x, 20, __float_as_uint(sc[0]), __float_as_uint(t));
+                    MH_CK(d != BOUND_ACCEPT || acc_x, 21, __float_as_uint(sc[0]), __float_as_uint(t));
+                    if ((d == BOUND_REJECT && acc_x) || (d == BOUND_ACCEPT && !acc_x)) {
+                        if (atomicCAS(&g_spec_ck[0], 0u, 1u) == 0u) {  // (the first one's inputs)
+                            g_spec_ck[1] = __float_as_uint(sc[0]);
+                            g_spec_ck[2] = __float_as_uint(t);
+                            g_spec_ck[3] = __float_as_uint(e);
+                            g_spec_ck[4] = __float_as_uint(cur_n.lo);
+                            g_spec_ck[5] = __float_as_uint(u_n);
+                            g_spec_ck[6] = (unsigned)d | ((unsigned)lane << 8) | ((unsigned)tr.dep << 16);
+                            g_spec_ck[7] = (unsigned)tr.cpar | ((unsigned)kb << 8) | ((unsigned)H << 16);
+                            g_spec_ck[8] = __float_as_uint(cur[0]);
+                            g_spec_ck[9] = (unsigned)done;
+                            g_spec_ck[10] = __float_as_uint(e0);
+                            g_spec_ck[11] = (unsigned)hf;
+                        }
+                    }
+                    mh_count_decision(d, true);
+                    atomicAdd(&g_check[5], 1u);
+                }
+#else
+                ab = __ballot(live && d == BOUND_ACCEPT);
+                ob = __ballot(live && d == BOUND_OPEN);
+#endif
+            }
         }
         // The realised path from the root: its nodes' steps commit; the configuration after
         // them is the last accepted node's (or the incoming one). A node the bound leaves open
