@@ -1623,6 +1623,10 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 12; ++k) stage(ch.aux)->cyc[k] = 0;
+        // the loop's shader cycles beside the constant 100 MHz counter: the clock it ran at
+        unsigned long long loop_c0 = 0, loop_r0 = 0;
+        MH_STAMP(loop_c0);
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(loop_r0) :: "memory");
 #endif
 #pragma clang loop unroll(disable)
         for (int it = 0; it < a.iterations; ++it) {
@@ -1811,6 +1815,15 @@ __global__ void __launch_bounds__(512) MH_OCC mh_kernel(LaunchArgs a) {
 #if MH_STAMPS
         if (writer)
             for (int k = 0; k < 12; ++k) atomicAdd(&g_phase_cycles[k], ch.aux->cyc[k]);
+        {
+            unsigned long long c1 = 0, r1 = 0;
+            MH_STAMP(c1);
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1) :: "memory");
+            if (writer) {
+                atomicAdd(&g_phase_cycles[12], c1 - loop_c0);
+                atomicAdd(&g_phase_cycles[13], r1 - loop_r0);
+            }
+        }
 #endif
 #if MH_CHECK
         if (!TRACK && FASTK_OF(L, NPL) && r == 0)  // a launch ends with exact current costs
@@ -2237,7 +2250,7 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_decisions(unsigne
 #if MH_STAMPS
 extern "C" __attribute__((visibility("default"))) int mh_debug_phase_cycles(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 12) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 14) ==
                    hipSuccess ? 0 : -1;
 }
 #endif

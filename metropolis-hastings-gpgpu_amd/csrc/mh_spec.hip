@@ -31,6 +31,11 @@ __device__ unsigned int g_spec_dbg_n;
 #if MH_STAMPS
 // cycles of the phases of a batch (0-11), then batches and committed steps (14, 15)
 __device__ unsigned long long g_spec_cycles[16];
+// per chain (the first 16,384): the loop's start and end on the 100 MHz counter, and where it ran
+// (HW_ID in the low word: wave, SIMD, CU, SH, SE; XCC_ID in the high word), its batches, exact
+// batches and refresh batches
+__device__ unsigned long long g_spec_place[6 * 16384];
+__device__ unsigned int g_spec_simd[4 * 16384];  // HW_ID of each wavefront of the chain
 #define SSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t) :: "memory"); cyc[k] += _t - t_last; t_last = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define SSTAMP(k) do { } while (0)
@@ -349,6 +354,10 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
 
     const int64_t chain = (int64_t)blockIdx.x;  // (the whole workgroup: one chain)
     if (chain >= a.n_chains) return;
+#if MH_STAMPS
+    if ((threadIdx.x & 63) == 0 && chain < 16384)  // where each of the chain's wavefronts runs
+        g_spec_simd[4 * chain + (threadIdx.x >> 6)] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
     // per half: the chain wavefront's LDS, then the list wavefront's; then the shared part
     auto X0of = [&](int h) __attribute__((always_inline)) {
         return reinterpret_cast<SpecW0*>(lds + kSpecHdrBytes + h * kSpecW0Bytes);
@@ -784,8 +793,11 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
     bool cur_exact = true;
     bool exact_next = !BOUND;
 #if MH_STAMPS
-    unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last;
+    unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last, rt0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
+    // the constant 100 MHz counter beside it: shader cycles / real time = the clock the chain ran at
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0) :: "memory");
+    const unsigned long long t_first = t_last;
 #endif
 #pragma clang loop unroll(disable)
     for (int done = 0;;) {
@@ -1280,6 +1292,22 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
 #endif
     }
 #if MH_STAMPS
+    {
+        unsigned long long rt1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1) :: "memory");
+        cyc[8] = t_last - t_first;  // shader cycles of the loop
+        cyc[9] = rt1 - rt0;         // 100 MHz ticks of the same span
+        if (lead && lane == 0 && chain < 16384) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // XCC_ID
+            g_spec_place[6 * chain + 0] = rt0;
+            g_spec_place[6 * chain + 1] = rt1;
+            g_spec_place[6 * chain + 2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+            g_spec_place[6 * chain + 3] = cyc[14];
+            g_spec_place[6 * chain + 4] = cyc[13];
+            g_spec_place[6 * chain + 5] = cyc[12];
+        }
+    }
     if (lead && lane == 0)  // (wave 0's timeline; its wait for wave 1 lands in "ordered sums")
         for (int k = 0; k < 16; ++k) atomicAdd(&g_spec_cycles[k], cyc[k]);
 #endif
@@ -1320,6 +1348,16 @@ extern "C" __attribute__((visibility("default"))) int mh_debug_spec(unsigned int
 #endif
 
 #if MH_STAMPS
+extern "C" __attribute__((visibility("default"))) int mh_debug_spec_place(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_place), sizeof(unsigned long long) * 6 * 16384) ==
+                   hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int mh_debug_spec_simd(unsigned int* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_simd), sizeof(unsigned int) * 4 * 16384) ==
+                   hipSuccess ? 0 : -1;
+}
 extern "C" __attribute__((visibility("default"))) int mh_debug_spec_cycles(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spec_cycles), sizeof(unsigned long long) * 16) != hipSuccess)

@@ -54,12 +54,13 @@ def main():
         return
     if s_kind == "speculative":  # one chain per wavefront, per-batch phases
         assert lib.mh_debug_spec_cycles(out) == 0
-        tot = sum(out[:12])  # ([12] refresh batches, [13] exact batches, [14], [15] counts)
+        tot = sum(out[:8])  # ([8] loop cycles, [9] its 100 MHz ticks, [12]-[15] counts)
         batches, steps = out[14], out[15]
         print(f"N={n} chains={chains} iters={iters} speculative acceptance={acc_rate:.4f} "
               f"steps per batch {steps / max(1, batches):.3f}; batches: {batches} "
-              f"(exact {out[13]}, of them refresh {out[12]})")
-        for name, v in zip(SPEC_PHASES, out[:12]):
+              f"(exact {out[13]}, of them refresh {out[12]}); shader clock over the loop "
+              f"{out[8] / max(1, out[9]) * 0.1:.3f} GHz (s_memtime / s_memrealtime)")
+        for name, v in zip(SPEC_PHASES, out[:8]):
             if not name:
                 continue
             print(f"  {name:24s} {100.0 * v / tot:6.2f}%   {v / max(1, batches):10.1f} cycles/batch"
@@ -84,6 +85,9 @@ def main():
               f"{out[9] / steps:.4f} ({out[9] / out[8]:.4f} of those evaluated), certain accept "
               f"on {out[10] / steps:.4f}; exact costs of the current configuration recomputed on "
               f"{out[11] / steps:.4f}")
+    if not delta and out[13]:  # the loop's shader cycles and 100 MHz ticks, summed over chains
+        print(f"  shader clock over the step loop {out[12] / out[13] * 0.1:.3f} GHz "
+              f"(s_memtime / s_memrealtime)")
     if delta and out[12]:  # counts (MH_STAMPS=2 builds): per step that reached the replay
         steps = chains * iters
         rep = max(1, out[12] - out[13] - out[14])
