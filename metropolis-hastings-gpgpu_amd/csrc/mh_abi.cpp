@@ -334,11 +334,13 @@ bool choose_geometry(int n, int c, int r, int device, int64_t n_chains, bool pla
     if (const char* e = getenv("MH_SPEC_H"))
         if (*e) g.spec_h = atoi(e) >= 2 ? 2 : 1;
     // Decisions on the bound (mh_spec.hip): the instance that takes them holds ~175 VGPRs, two
-    // wavefronts per SIMD (4 chains per CU at one half, 2 at two), and its batches trade the exact
-    // jobs and sums for fp32 estimates. Measured at N = 8 (ms per 1,000-step launch, bound / exact,
-    // profiles/r06/r06i_*): 256 chains 1.530 / 1.560, 1,024 chains 2.525 / 1.979. So up to two chains
-    // per CU. $MH_SPEC_BOUND=0/1 forces it.
-    g.spec_bound = n_chains <= 2LL * cus;
+    // wavefronts per SIMD (4 chains per CU at one half, 2 at two: the dispatcher then spreads a
+    // CU's wavefronts evenly over its SIMDs), and its batches trade the exact jobs and sums for
+    // fp32 estimates. Measured at N = 8 (ms per 1,000-step launch, bound / exact,
+    // profiles/r06/r06v_*): 256 chains 1.40 / 1.56, 1,024 chains (config 2) 1.73 / 1.98, 2,048
+    // chains 3.37-3.85 / 3.68 (two rounds of chains). So up to four chains per CU.
+    // $MH_SPEC_BOUND=0/1 forces it.
+    g.spec_bound = n_chains <= 4LL * cus;
     if (const char* e = getenv("MH_SPEC_BOUND"))
         if (*e) g.spec_bound = atoi(e) != 0;
     g.lay_ol = mh::make_lds_layout(n, c, r, g.L, true);

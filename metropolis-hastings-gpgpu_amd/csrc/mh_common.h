@@ -1361,13 +1361,15 @@ __device__ __forceinline__ double rel_pw_est(float4 e0, ObjP ps, ObjP pt, bool& 
 // The fp32 PairWiseAngle estimate from theta's estimate `tp` (atan2_est) and the target's pose
 // words, with its absolute allowance `eang`; `amb` near theta's wraps and the wrapped range's
 // switch, for a target rotation outside |rotY| < 16, or where the relationship takes no estimate.
-// e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts).
+// e1 = {(float)amin, (float)amax, 1 / norm, flags}, ea = e0.w (rel_est_consts). `flat`: the pair's
+// float y difference is zero and its x difference positive, so theta is exactly +-0 (atan2 of a
+// zero over a positive number, Kernel.cu:171-176) and takes no wrap: tp = 0 is then no ambiguity.
 __device__ __forceinline__ double rel_ang_est(float4 e1, float ea, ObjP atp, float tp, float& eang,
-                                              bool& amb) {
+                                              bool& amb, bool flat = false) {
 #pragma clang fp contract(fast)  // (fused: fewer roundings than the allowance counts)
     constexpr float U = 0x1p-24f, Y = (float)kTwoPI;
     const int fl = __float_as_int(e1.w);
-    amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || fabsf(tp) <= kDeltaTh;
+    amb |= (fl & RE_EXACT) != 0 || !(fabsf(atp.rotYf) < 16.0f) || (!flat && fabsf(tp) <= kDeltaTh);
     if (tp < 0.0f) tp = tp + Y;
     const float t = tp - atp.rotYf;
     amb |= fabsf(t) <= kDeltaTh;

@@ -785,13 +785,20 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
     // maxima as their screening estimates, the other terms exact -- and decides Accept where the
     // bound makes it certain. The realised path commits while its decisions are certain; at the
     // first open one it stops, and the next batch evaluates every node's exact costs (as every
-    // batch does without the bound), after a refresh batch that makes the current costs exact
-    // when a certain acceptance left them an interval. The carried terms may be estimates
+    // batch does without the bound); when a certain acceptance left the current costs an interval,
+    // that batch's last node evaluates the incoming configuration instead (a refresh), and the
+    // root's decisions compare with its exact total. The carried terms may be estimates
     // (allowances efp_c, ea0_c, ea1_c: 0 when exact); an exact batch evaluates them exactly.
     float efp_c = 0.0f, ea0_c = 0.0f, ea1_c = 0.0f;
     CostIv cur_iv{cur[0], cur[0]};
     bool cur_exact = true;
     bool exact_next = !BOUND;
+    // Where the bound keeps leaving nodes open -- a chain whose configuration sits near a branch of
+    // an estimate, say -- its stops cost more than the bound saves, and the launch waits for that
+    // chain. An open stop within 4 bound batches of the previous one doubles a run of exact
+    // batches that follows it (up to 64); a later one resets it (exact_run: exact batches still to
+    // run after the one the stop asks for; since_open: bound batches since the last stop).
+    int exact_run = 0, backoff = 1, since_open = 0;
 #if MH_STAMPS
     unsigned long long cyc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last, rt0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last) :: "memory");
@@ -808,17 +815,18 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             break;
         }
         // (check builds: exact costs and the bound in every batch, decisions on the exact costs)
-        const bool exact_b = exact_next || finish || !BOUND || MH_CHECK;
+        const bool exact_b = exact_next || exact_run > 0 || finish || !BOUND || MH_CHECK;
         const bool bound_b = !exact_b || MH_CHECK;
-        // a launch ends, and an exact batch starts, with the current configuration's exact
-        // costs: when a certain acceptance left them an interval, a refresh batch (no steps, every
-        // node the incoming configuration) evaluates them first
+        // a launch ends, and an exact batch decides, with the current configuration's exact
+        // costs: when a certain acceptance left them an interval, node NN - 1 evaluates the
+        // incoming configuration (the tree without that node this batch)
         const bool refresh = exact_b && !cur_exact;
         if ((++batches & 31u) == 0u)
             set_tree((float)(accepted + 2u) / (float)(done + 5));
+        const int dep_g = refresh && K * hf + g == NN - 1 ? -1 : my_dep;  // (-1: nothing applied)
         // steps this batch can reach: the tree's depth, the launch's remaining steps, the
         // records wave 1 has written (0: a round that only waits for it)
-        const int kb = refresh ? 0 : min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
+        const int kb = min(min(tr.maxdep + 1, a.iterations - done), (int)(prod_seen - cons));
         if (lane < kb) {
             const StepRec& q = rec(cons + (unsigned int)lane);
             r_code = q.code;
@@ -832,7 +840,7 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
         double sx = cx, sy = cy, sry = cry;
         bool moved = false;  // this lane's object differs from the incoming state
         apply(sx, sy, sry, moved, kb, [&](int i) __attribute__((always_inline)) {
-            return i == my_dep || (i < my_dep && ((my_hist >> i) & 1));
+            return i == dep_g || (i < dep_g && ((my_hist >> i) & 1));
         });
         const float xf = (float)sx, yf = (float)sy, ryf = (float)sry;
         if (r < n) {
@@ -897,7 +905,9 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                     const ObjP as = PGg[rc.as], atp = PGg[rc.at];
                     const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
                     amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
-                    an = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
+                    // (a pair on one horizontal line, e.g. both clamped to a wall: theta is exactly 0)
+                const bool flat = ay == 0.0f && ax > 0.0f;
+                an = rel_ang_est(e1, e0.w, atp, flat ? 0.0f : atan2_est(ay, ax), ea, amb, flat);
                     if (amb) pw = __builtin_nan("");  // (an estimate that cannot vouch for its branch:
                                                       // the node is open, its exact terms next batch)
                 };
@@ -1091,8 +1101,10 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             t = t + sc[7];
             sc[0] = t;
             const float cp_tot = shfl_f(sc[0], cpar_l);
-            const float cur_n = tr.cpar == kNone ? cur[0] : cp_tot;
-            const bool acc_n = lane < NN && tr.dep < kb &&
+            // (a refresh: the root's current total is node NN - 1's, the incoming configuration's)
+            const float cur0 = refresh ? readlane_f(sc[0], NN - 1) : cur[0];
+            const float cur_n = tr.cpar == kNone ? cur0 : cp_tot;
+            const bool acc_n = lane < NN && tr.dep < kb && !(refresh && lane == NN - 1) &&
                                accept_u(u_n, kBeta * ((double)sc[0] - (double)cur_n));
             ab = __ballot(acc_n);
         }
@@ -1163,7 +1175,7 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
         unsigned int acc_steps = 0;
 #pragma unroll
         for (int d = 0; d < NN; ++d) {
-            if (node == kNone || d >= kb) break;
+            if (node == kNone || (refresh && node == NN - 1) || d >= kb) break;
             if ((ob >> node) & 1ull) {
                 exact_next = true;
                 break;
@@ -1177,11 +1189,22 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
             }
             node = __builtin_amdgcn_readlane(an ? tr.cha : tr.chr, node);
         }
-        if (exact_b) exact_next = !BOUND;
+        if constexpr (BOUND && !MH_CHECK) {
+            if (exact_b) {
+                if (exact_next) exact_next = false;
+                else if (exact_run > 0) --exact_run;
+            } else if (exact_next) {  // this bound batch stopped at an open node
+                backoff = since_open < 4 ? min(2 * backoff, 64) : 1;
+                exact_run = backoff - 1;
+                since_open = 0;
+            } else {
+                ++since_open;
+            }
+        }
         if (refresh) {
-            // node 0 evaluated the incoming configuration: its exact costs and terms are the
-            // current ones
-            const double* sl = streams_of(0).ptr();
+            // node NN - 1 evaluated the incoming configuration: its exact costs and terms are the
+            // current ones (until a committed node's replace them below)
+            const double* sl = streams_of((NN - 1) / K).ptr() + ((NN - 1) % K) * S_W0;
             if (r < n) cph = (float)(-sl[S_FP + r]);
             if (r < nr) {
                 rpw0 = -sl[S_PW + r];
@@ -1192,7 +1215,7 @@ __global__ void __launch_bounds__(128 * H) mh_spec_kernel(LaunchArgs a) {
                 rang1 = -sl[S_ANG + r + GL];
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], 0);
+            for (int k = 0; k < 8; ++k) cur[k] = readlane_f(sc[k], NN - 1);
             cur_iv = CostIv{cur[0], cur[0]};
             cur_exact = true;
             efp_c = ea0_c = ea1_c = 0.0f;

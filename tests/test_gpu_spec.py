@@ -111,18 +111,17 @@ def test_spec_is_the_default_for_few_small_chains(mh, hiplib, monkeypatch):
         assert s.step_kernel()[2] == "speculative"
     # the 16-node instance up to two chains per CU, the 8-node one beyond (config 2's 1,024
     # chains on 256 CUs)
-    # chains per CU; the instance deciding on the bound (two wavefronts per SIMD) up to two
-    # chains per CU, the exact one (98 VGPRs; LDS-bound residency) beyond
+    # chains per CU; the instance deciding on the bound (two wavefronts per SIMD) up to four
+    # chains per CU (config 2), the exact one (98 VGPRs; LDS-bound residency) beyond
     with mh.Session(mh.synthetic_room(8), 2 * cus, seed=1) as s:
         assert s.step_kernel() == (256, 1, "speculative") and s.occupancy() == 2
     with mh.Session(mh.synthetic_room(8), 2 * cus + 1, seed=1) as s:
+        assert s.step_kernel() == (128, 1, "speculative") and s.occupancy() == 4
+    with mh.Session(mh.synthetic_room(8), 4 * cus + 1, seed=1) as s:
         assert s.step_kernel() == (128, 1, "speculative") and s.occupancy() >= 5
     monkeypatch.setenv("MH_SPEC_BOUND", "0")
     with mh.Session(mh.synthetic_room(8), 2 * cus, seed=1) as s:
         assert s.step_kernel() == (256, 1, "speculative") and s.occupancy() == 4
-    monkeypatch.setenv("MH_SPEC_BOUND", "1")
-    with mh.Session(mh.synthetic_room(8), 4 * cus, seed=1) as s:
-        assert s.step_kernel() == (128, 1, "speculative") and s.occupancy() == 4
     monkeypatch.delenv("MH_SPEC_BOUND")
     with mh.Session(mh.synthetic_room(8), 1024, seed=1, track=1) as s:  # (plain family only)
         assert s.step_kernel()[2] != "speculative"

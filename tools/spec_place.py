@@ -72,6 +72,8 @@ def main():
               f"{sum(nb[i] for i in sel) / k:8.1f}, exact {sum(ne[i] for i in sel) / k:7.1f}, "
               f"refresh {sum(nr[i] for i in sel) / k:7.1f}, us per batch "
               f"{sum(dur[i] / max(1, nb[i]) for i in sel) / k:.3f}")
+    print("  slowest chains (us, batches, exact, refresh): " + "; ".join(
+        f"{i}: {dur[i]:.0f}, {nb[i]}, {ne[i]}, {nr[i]}" for i in order[-8:][::-1]))
     # the SIMDs of the chain's wavefronts (HW_ID bits 5:4), and the waves of this launch per SIMD
     sb = (C.c_uint * (4 * 16384))()
     assert lib.mh_debug_spec_simd(sb) == 0
