@@ -267,8 +267,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
             rpw = rel_pw_est(e0, ps, pt, amb);
             const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
             amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= TINY);
-            const bool flat = ay == 0.0f && ax > 0.0f;  // (theta exactly 0: rel_ang_est)
-            rang = rel_ang_est(e1, e0.w, atp, flat ? 0.0f : atan2_est(ay, ax), eang, amb, flat);
+            rang = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), eang, amb);
         }
         return;
     }
@@ -301,8 +300,7 @@ __device__ __forceinline__ void approx_terms(const ChainPtrs& ch, const DevRoom&
     if (obj) cph = cph_est(at, p, ambo);
     if (rel) {
         amb |= tiny;
-        const bool flat = ay == 0.0f && ax > 0.0f;  // (theta exactly 0: rel_ang_est)
-        rang = rel_ang_est(e1, e0.w, atp, flat ? 0.0f : a1, eang, amb, flat);
+        rang = rel_ang_est(e1, e0.w, atp, a1, eang, amb);
     }
 }
 

@@ -511,8 +511,7 @@ __device__ __forceinline__ void rels_delta(const DeltaPtrs& ch, int nr, int ka, 
                 const float ay = as.yf - atp.yf, ax = as.xf - atp.xf;
                 amb |= !(fmaxf(fabsf(ay), fabsf(ax)) >= 0x1p-100f);
                 float ea = 0.0f;
-                const bool flat = ay == 0.0f && ax > 0.0f;  // (theta exactly 0: rel_ang_est)
-                tang = rel_ang_est(e1, e0.w, atp, flat ? 0.0f : atan2_est(ay, ax), ea, amb, flat);
+                tang = rel_ang_est(e1, e0.w, atp, atan2_est(ay, ax), ea, amb);
                 const unsigned bit = 1u << u;
                 est->rel = amb ? (est->rel & ~bit) : (est->rel | bit);
                 if (u == 0) est->eang[0] = ea;
